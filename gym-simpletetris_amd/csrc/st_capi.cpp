@@ -1,0 +1,259 @@
+// st_capi.cpp -- extern "C" boundary of the batched SimpleTetris engine.
+// Declared in include/simpletetris.h; each entry point cites the reference
+// method it replaces there.  Owns the device state; launches the kernels of
+// st_kernels.hip on the caller's stream.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "st_internal.h"
+
+struct st_ctx {
+    st_config cfg;
+    int device;
+    int64_t n;
+    int64_t stride;
+    bool seeded;
+    bool reset_once;
+    uint32_t *board;
+    uint32_t *piece;
+    int32_t *stats;
+    uint32_t *mt;
+};
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+    return fail(ST_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define ST_HIP(call)                                   \
+    do {                                               \
+        hipError_t _e = (call);                        \
+        if (_e != hipSuccess) return hip_fail(_e, #call); \
+    } while (0)
+
+// Make the context's device current for the duration of a call.
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = true;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+st::KParams params(const st_ctx *c) {
+    st::KParams p{};
+    p.W = c->cfg.width;
+    p.H = c->cfg.height;
+    p.lock_mod = (c->cfg.lock_delay > 0 ? c->cfg.lock_delay : 0) + 1;
+    p.flags = c->cfg.flags;
+    p.autoreset = c->cfg.autoreset;
+    p.n = c->n;
+    p.stride = c->stride;
+    p.board = c->board;
+    p.piece = c->piece;
+    p.stats = c->stats;
+    p.mt = c->mt;
+    return p;
+}
+
+void free_state(st_ctx *c) {
+    if (c->board) (void)hipFree(c->board);
+    if (c->piece) (void)hipFree(c->piece);
+    if (c->stats) (void)hipFree(c->stats);
+    if (c->mt) (void)hipFree(c->mt);
+    c->board = c->piece = c->mt = nullptr;
+    c->stats = nullptr;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *st_last_error(void) { return g_err; }
+int st_abi_version(void) { return ST_ABI_VERSION; }
+
+int st_create(st_ctx **out, const st_config *cfg, int device, int64_t n_envs) {
+    g_err[0] = 0;
+    if (!out || !cfg) return fail(ST_EINVAL, "st_create: null argument");
+    *out = nullptr;
+    if (cfg->width < 4 || cfg->width > st::kMaxW)
+        return fail(ST_EINVAL, "width %d outside [4, %d]", cfg->width, st::kMaxW);
+    if (cfg->height < 4 || cfg->height > st::kMaxH)
+        return fail(ST_EINVAL, "height %d outside [4, %d]", cfg->height, st::kMaxH);
+    if (cfg->lock_delay > 32766) return fail(ST_EINVAL, "lock_delay %d > 32766", cfg->lock_delay);
+    if (cfg->flags & ~0xFFu) return fail(ST_EINVAL, "unknown flag bits 0x%x", cfg->flags);
+    if (cfg->autoreset != ST_AUTORESET_NONE && cfg->autoreset != ST_AUTORESET_SAME_STEP)
+        return fail(ST_EINVAL, "autoreset %d unknown", cfg->autoreset);
+    if (n_envs < 1 || n_envs > (int64_t(1) << 31))
+        return fail(ST_EINVAL, "n_envs %lld outside [1, 2^31]", (long long)n_envs);
+    int ndev = 0;
+    ST_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(ST_EINVAL, "device %d of %d", device, ndev);
+    DeviceGuard g(device);
+    if (!g.ok) return fail(ST_EHIP, "hipSetDevice(%d) failed", device);
+
+    st_ctx *c = new st_ctx();
+    c->cfg = *cfg;
+    c->device = device;
+    c->n = n_envs;
+    c->stride = (n_envs + st::kWave - 1) / st::kWave * st::kWave;
+    const size_t sd = (size_t)c->stride;
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = hipMalloc(&c->board, sd * cfg->width * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&c->piece, sd * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&c->stats, sd * ST_NSTAT * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(&c->mt, sd * st::kMtN * sizeof(uint32_t));
+    if (e != hipSuccess) {
+        free_state(c);
+        delete c;
+        return fail(ST_ENOMEM, "st_create: hipMalloc failed: %s", hipGetErrorString(e));
+    }
+    *out = c;
+    return ST_OK;
+}
+
+int st_destroy(st_ctx *c) {
+    if (!c) return ST_OK;
+    DeviceGuard g(c->device);
+    (void)hipDeviceSynchronize();
+    free_state(c);
+    delete c;
+    return ST_OK;
+}
+
+int st_seed(st_ctx *c, const uint64_t *seeds_host, st_stream stream) {
+    if (!c || !seeds_host) return fail(ST_EINVAL, "st_seed: null argument");
+    DeviceGuard g(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    // padding envs get seeds too (they run, unreported, in the last wave)
+    uint64_t *d_seeds = nullptr;
+    ST_HIP(hipMalloc(&d_seeds, (size_t)c->stride * sizeof(uint64_t)));
+    hipError_t e = hipMemcpyAsync(d_seeds, seeds_host, (size_t)c->n * sizeof(uint64_t),
+                                  hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && c->stride > c->n)
+        e = hipMemsetAsync(d_seeds + c->n, 0, (size_t)(c->stride - c->n) * sizeof(uint64_t), s);
+    st::KParams p = params(c);
+    p.seeds = d_seeds;
+    if (e == hipSuccess) e = st::launch_seed(p, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(d_seeds);
+    if (e != hipSuccess) return hip_fail(e, "st_seed");
+    c->seeded = true;
+    return ST_OK;
+}
+
+int st_reset(st_ctx *c, const uint8_t *d_mask, st_stream stream) {
+    if (!c) return fail(ST_EINVAL, "st_reset: null context");
+    if (!c->seeded) return fail(ST_ESTATE, "st_reset before st_seed");
+    DeviceGuard g(c->device);
+    st::KParams p = params(c);
+    p.mask = d_mask;
+    ST_HIP(st::launch_reset(p, (hipStream_t)stream));
+    if (!d_mask) c->reset_once = true;
+    return ST_OK;
+}
+
+static int step_impl(st_ctx *c, const uint8_t *d_actions, uint32_t *d_obs, float *d_obs_f32,
+                     int32_t *d_reward, uint8_t *d_done, st_stream stream) {
+    if (!c || !d_actions) return fail(ST_EINVAL, "st_step: null argument");
+    if (!c->seeded || !c->reset_once)
+        return fail(ST_ESTATE, "st_step before st_seed + st_reset (tetris_env.py:244 needs an anchor)");
+    DeviceGuard g(c->device);
+    st::KParams p = params(c);
+    p.actions = d_actions;
+    p.obs = d_obs;
+    p.obs_f32 = d_obs_f32;
+    p.reward = d_reward;
+    p.done = d_done;
+    ST_HIP(st::launch_step(p, (hipStream_t)stream));
+    return ST_OK;
+}
+
+int st_step(st_ctx *c, const uint8_t *d_actions, uint32_t *d_obs, int32_t *d_reward,
+            uint8_t *d_done, st_stream stream) {
+    return step_impl(c, d_actions, d_obs, nullptr, d_reward, d_done, stream);
+}
+
+int st_step_f32(st_ctx *c, const uint8_t *d_actions, uint32_t *d_obs, float *d_obs_f32,
+                int32_t *d_reward, uint8_t *d_done, st_stream stream) {
+    if (!d_obs_f32) return fail(ST_EINVAL, "st_step_f32: null d_obs_f32");
+    return step_impl(c, d_actions, d_obs, d_obs_f32, d_reward, d_done, stream);
+}
+
+int st_obs_to_f32(st_ctx *c, const uint32_t *d_obs, float *d_out, st_stream stream) {
+    if (!c || !d_obs || !d_out) return fail(ST_EINVAL, "st_obs_to_f32: null argument");
+    DeviceGuard g(c->device);
+    ST_HIP(st::launch_obs_f32(params(c), d_obs, d_out, (hipStream_t)stream));
+    return ST_OK;
+}
+
+int st_render(st_ctx *c, uint32_t *d_obs, st_stream stream) {
+    if (!c || !d_obs) return fail(ST_EINVAL, "st_render: null argument");
+    if (!c->seeded) return fail(ST_ESTATE, "st_render before st_seed");
+    DeviceGuard g(c->device);
+    st::KParams p = params(c);
+    p.obs = d_obs;
+    ST_HIP(st::launch_render(p, (hipStream_t)stream));
+    return ST_OK;
+}
+
+int st_grayscale(st_ctx *c, const uint32_t *d_obs, int32_t size, int32_t channels, int32_t as_u8,
+                 void *d_out, st_stream stream) {
+    if (!c || !d_obs || !d_out) return fail(ST_EINVAL, "st_grayscale: null argument");
+    if (channels != 1 && channels != 3) return fail(ST_EINVAL, "channels %d not 1 or 3", channels);
+    const int lim = c->cfg.width > c->cfg.height ? c->cfg.width : c->cfg.height;
+    const int gap = size / 100 + 1;
+    if (size < 8 || size > 4096 || (size - 2 * gap) / lim - gap < 1)
+        return fail(ST_EINVAL, "st_grayscale: size %d too small for a %dx%d board", size,
+                    c->cfg.width, c->cfg.height);
+    DeviceGuard g(c->device);
+    ST_HIP(st::launch_grayscale(params(c), d_obs, size, channels, as_u8, d_out, (hipStream_t)stream));
+    return ST_OK;
+}
+
+int st_copy(void *dst, const void *src, int64_t bytes, st_stream stream) {
+    if (bytes < 0 || ((!dst || !src) && bytes)) return fail(ST_EINVAL, "st_copy: bad argument");
+    if (!bytes) return ST_OK;
+    ST_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDefault, (hipStream_t)stream));
+    return ST_OK;
+}
+
+int st_state(st_ctx *c, st_state_views *out) {
+    if (!c || !out) return fail(ST_EINVAL, "st_state: null argument");
+    out->board = c->board;
+    out->piece = c->piece;
+    out->stats = c->stats;
+    out->mt = c->mt;
+    out->n_envs = c->n;
+    out->stride = c->stride;
+    out->width = c->cfg.width;
+    out->height = c->cfg.height;
+    return ST_OK;
+}
+
+int st_gen_actions(uint8_t *d_out, int64_t n, int64_t t, uint64_t seed, int64_t global_offset,
+                   st_stream stream) {
+    if (!d_out && n > 0) return fail(ST_EINVAL, "st_gen_actions: null output");
+    if (n < 0 || t < 0) return fail(ST_EINVAL, "st_gen_actions: negative size/time");
+    ST_HIP(st::launch_gen_actions(d_out, n, t, seed, global_offset, (hipStream_t)stream));
+    return ST_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,48 @@
+// Internal declarations shared by the HIP kernels and the C-ABI layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "simpletetris.h"
+
+namespace st {
+
+constexpr int kWave = 64;      // one env per lane, one wave per workgroup
+constexpr int kPad = 4;        // wall columns on each side of the LDS board
+constexpr int kMaxW = 32;
+constexpr int kMaxH = 28;
+constexpr int kMtN = 624;
+
+struct KParams {
+    int32_t W, H;
+    int32_t lock_mod;   // max(lock_delay, 0) + 1   (tetris_env.py:175)
+    uint32_t flags;
+    int32_t autoreset;
+    int64_t n;          // real envs
+    int64_t stride;     // padded env count (multiple of 64) = SoA row stride
+    // state
+    uint32_t *board;    // [W][stride]
+    uint32_t *piece;    // [stride]
+    int32_t *stats;     // [ST_NSTAT][stride]
+    uint32_t *mt;       // [stride][624]
+    // io
+    const uint8_t *actions;  // [n]
+    const uint8_t *mask;     // [n] (reset) or null
+    const uint64_t *seeds;   // [stride] (seed)
+    uint32_t *obs;           // [W][n]
+    float *obs_f32;          // [n][W][H]
+    int32_t *reward;         // [n]
+    uint8_t *done;           // [n]
+};
+
+hipError_t launch_seed(const KParams &p, hipStream_t s);
+hipError_t launch_reset(const KParams &p, hipStream_t s);
+hipError_t launch_step(const KParams &p, hipStream_t s);
+hipError_t launch_obs_f32(const KParams &p, const uint32_t *obs, float *out, hipStream_t s);
+hipError_t launch_render(const KParams &p, hipStream_t s);
+hipError_t launch_grayscale(const KParams &p, const uint32_t *obs, int size, int channels,
+                            int as_u8, void *out, hipStream_t s);
+hipError_t launch_gen_actions(uint8_t *out, int64_t n, int64_t t, uint64_t seed, int64_t off,
+                              hipStream_t s);
+
+}  // namespace st

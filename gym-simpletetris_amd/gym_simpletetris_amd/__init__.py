@@ -1,0 +1,37 @@
+"""gym_simpletetris_amd -- MI355X-native batched SimpleTetris engine.
+
+Drop-in for gym-simpletetris' step path (reference:
+gym_simpletetris/__init__.py:1-6 registers 'SimpleTetris-v0' ->
+gym_simpletetris.envs:TetrisEnv).  `make('SimpleTetris-v0', **kwargs)` returns
+the single-env reference surface; `make('SimpleTetris-v0', num_envs=N, ...)`
+or `make('SimpleTetrisVec-v0', ...)` the batched one.  When gym or gymnasium
+is importable the ids are registered there too.
+"""
+from .engine import SHAPE_NAMES, TetrisBatch  # noqa: F401
+from .envs import TetrisEnv, TetrisVecEnv  # noqa: F401
+
+__version__ = "0.1.0"
+
+ENV_IDS = ("SimpleTetris-v0", "SimpleTetrisVec-v0")
+
+
+def make(env_id: str = "SimpleTetris-v0", **kwargs):
+    """gym.make equivalent for the two registered ids."""
+    if env_id not in ENV_IDS:
+        raise KeyError(f"unknown env id {env_id!r}; known: {ENV_IDS}")
+    if env_id == "SimpleTetrisVec-v0" or "num_envs" in kwargs:
+        return TetrisVecEnv(kwargs.pop("num_envs", 1), **kwargs)
+    return TetrisEnv(**kwargs)
+
+
+def _register():
+    for modname in ("gym", "gymnasium"):
+        try:  # pragma: no cover - neither is installed in the build image
+            mod = __import__(modname)
+            mod.envs.registration.register(id="SimpleTetris-v0",
+                                           entry_point="gym_simpletetris_amd.envs:TetrisEnv")
+        except Exception:  # noqa: BLE001
+            pass
+
+
+_register()

@@ -1,0 +1,95 @@
+"""Multi-GPU sharding of the env batch: one process per GPU.
+
+Envs are independent state machines (the reference's only shared state is the
+global `random`, tetris_env.py:187, which the engine replaces by per-env
+MT19937 streams), so the batch shards by contiguous global index with NO
+collective in the step.  Seeds and synthetic actions are keyed by the global
+env index, so results are identical at any GPU count.
+
+The one exchange the north star names -- delivering every shard's packed
+obs / reward / done to rank 0 -- is `gather_outputs`: one torch.distributed
+gather (RCCL over xGMI with the 'nccl' backend; gloo on CPU in the tests) of a
+single contiguous int32 buffer per rank, laid out [W + 2][n_local]:
+rows 0..W-1 packed obs words, row W reward, row W+1 done bytes.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n_global: int, world: int, rank: int) -> Tuple[int, int]:
+    """(offset, count) of rank's contiguous block; the first n_global % world
+    ranks get one extra env."""
+    if not 0 <= rank < world:
+        raise ValueError(f"rank {rank} outside world {world}")
+    base, rem = divmod(n_global, world)
+    count = base + (1 if rank < rem else 0)
+    offset = rank * base + min(rank, rem)
+    return offset, count
+
+
+def output_buffer(width: int, n_local: int, device) -> torch.Tensor:
+    """The per-rank packed output buffer [W + 2][n_local] int32."""
+    return torch.zeros((width + 2, n_local), dtype=torch.int32, device=device)
+
+
+def buffer_views(buf: torch.Tensor, width: int):
+    """(obs [W][n] int32, reward [n] int32, done [n] uint8) views into buf."""
+    n = buf.shape[1]
+    done = buf[width + 1].view(torch.uint8)[:n]
+    return buf[:width], buf[width], done
+
+
+def gather_outputs(buf: torch.Tensor, group=None, dst: int = 0) -> Optional[List[torch.Tensor]]:
+    """Gather every rank's packed buffer to `dst` (equal shard sizes)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    bufs = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
+    dist.gather(buf, gather_list=bufs, dst=dst, group=group)
+    return bufs
+
+
+def assemble(bufs: List[torch.Tensor], width: int):
+    """Rank-0 side: concatenate gathered buffers into global (obs [W][N],
+    reward [N], done [N]) in global env order."""
+    obs = torch.cat([b[:width] for b in bufs], dim=1)
+    reward = torch.cat([b[width] for b in bufs])
+    done = torch.cat([buffer_views(b, width)[2] for b in bufs])
+    return obs, reward, done
+
+
+class ShardedTetris:
+    """This rank's shard of a global batch of `n_global` envs."""
+
+    def __init__(self, n_global: int, seed: int = 0, rank: Optional[int] = None,
+                 world: Optional[int] = None, device=None, **engine_kwargs):
+        from .engine import TetrisBatch
+        self.rank = dist.get_rank() if rank is None else rank
+        self.world = dist.get_world_size() if world is None else world
+        self.offset, self.n = shard_range(n_global, self.world, self.rank)
+        self.engine = TetrisBatch(self.n, device=device,
+                                  seeds=[seed + self.offset + e for e in range(self.n)],
+                                  **engine_kwargs)
+        self.buf = output_buffer(self.engine.width, self.n, self.engine.device)
+        self._obs, self._rew, self._done = buffer_views(self.buf, self.engine.width)
+
+    def reset(self):
+        self.engine.reset()
+
+    def step(self, actions: torch.Tensor):
+        """Step the shard, writing straight into the gather buffer."""
+        from . import _lib as C
+        import ctypes
+        e = self.engine
+        with torch.cuda.device(e.device):
+            C.check(e._L.st_step(e._ctx, ctypes.c_void_p(actions.data_ptr()),
+                                 ctypes.c_void_p(self._obs.data_ptr()),
+                                 ctypes.c_void_p(self._rew.data_ptr()),
+                                 ctypes.c_void_p(self._done.data_ptr()), e._stream()))
+        return self._obs, self._rew, self._done
+
+    def gather(self, dst: int = 0):
+        return gather_outputs(self.buf, dst=dst)

@@ -1,0 +1,255 @@
+"""TetrisBatch: N independent SimpleTetris engines resident on one MI355X.
+
+Host mirror of TetrisEngine (/root/reference/gym_simpletetris/envs/tetris_env.py:125-335)
+for N envs at once.  All game logic runs in the HIP kernels of
+libsimpletetris.so (csrc/st_kernels.hip); this class only owns the context,
+the output buffers (torch tensors on the device) and the stream plumbing.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib as C
+
+SHAPE_NAMES = ("T", "J", "L", "Z", "S", "I", "O")  # tetris_env.py:19
+
+# Reference constructor kwargs (TetrisEngine.__init__ / TetrisEnv.__init__).
+SCORING_KWARGS = ("reward_step", "penalise_height", "penalise_height_increase",
+                  "advanced_clears", "high_scoring", "penalise_holes",
+                  "penalise_holes_increase")
+
+
+def _stream_ptr(device: torch.device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[ctypes.c_void_p]:
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class TetrisBatch:
+    """Batched engine.  `autoreset`: 'none' (exact reference semantics; the
+    caller resets done envs, like `if done: env.reset()`) or 'same_step'
+    (clear() runs inside the step kernel for envs that died)."""
+
+    def __init__(self, n_envs: int, width: int = 10, height: int = 20, lock_delay: int = 0,
+                 step_reset: bool = False, reward_step: bool = False,
+                 penalise_height: bool = False, penalise_height_increase: bool = False,
+                 advanced_clears: bool = False, high_scoring: bool = False,
+                 penalise_holes: bool = False, penalise_holes_increase: bool = False,
+                 autoreset: str = "none", device=None, seeds: Optional[Sequence[int]] = None):
+        self._L = C.load()
+        if not torch.cuda.is_available():
+            raise RuntimeError("TetrisBatch needs a ROCm GPU (no CPU fallback by design)")
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise ValueError(f"device must be a GPU, got {device}")
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        if autoreset not in C.AUTORESET:
+            raise ValueError(f"autoreset must be one of {sorted(C.AUTORESET)}")
+        kw = dict(reward_step=reward_step, penalise_height=penalise_height,
+                  penalise_height_increase=penalise_height_increase,
+                  advanced_clears=advanced_clears, high_scoring=high_scoring,
+                  penalise_holes=penalise_holes,
+                  penalise_holes_increase=penalise_holes_increase, step_reset=step_reset)
+        flags = 0
+        for k, v in kw.items():
+            if v:
+                flags |= C.FLAGS[k]
+        self.n = int(n_envs)
+        self.width, self.height = int(width), int(height)
+        self.lock_delay = int(lock_delay)
+        self.flags = flags
+        self.kwargs = dict(kw, lock_delay=self.lock_delay, width=self.width, height=self.height)
+        self.autoreset = autoreset
+        self.device = device
+        cfg = C.Config(self.width, self.height, self.lock_delay, flags, C.AUTORESET[autoreset])
+        ctx = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            C.check(self._L.st_create(ctypes.byref(ctx), ctypes.byref(cfg), device.index, self.n))
+        self._ctx = ctx
+        v = C.StateViews()
+        C.check(self._L.st_state(ctx, ctypes.byref(v)))
+        self._views = v
+        self.stride = int(v.stride)
+        W, n = self.width, self.n
+        # Reused output buffers (valid until the next step, like a vec-env obs buffer).
+        self.obs = torch.zeros((W, n), dtype=torch.int32, device=device)  # packed u32 bits
+        self.obs_f32: Optional[torch.Tensor] = None
+        self.reward = torch.zeros(n, dtype=torch.int32, device=device)
+        self.done = torch.zeros(n, dtype=torch.bool, device=device)
+        self._act = torch.zeros(n, dtype=torch.uint8, device=device)
+        self._seeded = False
+        if seeds is not None:
+            self.seed(seeds)
+
+    # ------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "_ctx", None) is not None and self._ctx.value:
+            self._L.st_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self):
+        return _stream_ptr(self.device)
+
+    def seed(self, seeds: Sequence[int]):
+        """random.seed(seeds[e]) for each env (CPython MT19937 init_by_array)."""
+        s = np.asarray([int(x) for x in seeds], dtype=object)
+        if len(s) != self.n:
+            raise ValueError(f"need {self.n} seeds, got {len(s)}")
+        arr = np.empty(self.n, np.uint64)
+        for i, x in enumerate(s):
+            x = abs(int(x))  # random.seed uses abs() of an int seed
+            if x >= 1 << 64:
+                raise ValueError("seeds must fit in 64 bits")
+            arr[i] = x
+        with torch.cuda.device(self.device):
+            C.check(self._L.st_seed(self._ctx, ctypes.c_void_p(arr.ctypes.data), self._stream()))
+        self._seeded = True
+
+    def _as_dev_u8(self, x, name) -> torch.Tensor:
+        if isinstance(x, torch.Tensor):
+            t = x.to(device=self.device, dtype=torch.uint8)
+        else:
+            t = torch.as_tensor(np.asarray(x, dtype=np.uint8), device=self.device)
+        if t.numel() != self.n:
+            raise ValueError(f"{name} must have {self.n} entries, got {t.numel()}")
+        return t.contiguous()
+
+    def reset(self, mask=None):
+        """TetrisEngine.clear() on every env (mask None) or where mask != 0."""
+        if not self._seeded:
+            raise RuntimeError("seed() before reset()")
+        m = None if mask is None else self._as_dev_u8(mask, "mask")
+        with torch.cuda.device(self.device):
+            C.check(self._L.st_reset(self._ctx, _ptr(m), self._stream()))
+
+    def step(self, actions, obs: str = "packed"):
+        """One TetrisEngine.step on every env.  obs: 'packed' (u32 [W][n]),
+        'f32' (also float32 [n][W][H], fused in the kernel) or 'none'.
+        Returns (obs, reward int32 [n], done bool [n]) -- reused buffers."""
+        a = actions if (isinstance(actions, torch.Tensor) and actions.dtype == torch.uint8
+                        and actions.device == self.device and actions.is_contiguous()) \
+            else self._as_dev_u8(actions, "actions")
+        s = self._stream()
+        with torch.cuda.device(self.device):
+            if obs == "f32":
+                if self.obs_f32 is None:
+                    self.obs_f32 = torch.zeros((self.n, self.width, self.height),
+                                               dtype=torch.float32, device=self.device)
+                C.check(self._L.st_step_f32(self._ctx, _ptr(a), _ptr(self.obs), _ptr(self.obs_f32),
+                                            _ptr(self.reward), _ptr(self.done), s))
+                return self.obs_f32, self.reward, self.done
+            C.check(self._L.st_step(self._ctx, _ptr(a), _ptr(self.obs) if obs == "packed" else None,
+                                    _ptr(self.reward), _ptr(self.done), s))
+        return (self.obs if obs == "packed" else None), self.reward, self.done
+
+    # ------------------------------------------------------------ observations
+    def obs_to_f32(self, packed: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Packed obs -> float32 [n][W][H] (the reference's np.float32 board)."""
+        packed = self.obs if packed is None else packed
+        out = torch.empty((self.n, self.width, self.height), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            C.check(self._L.st_obs_to_f32(self._ctx, _ptr(packed), _ptr(out), self._stream()))
+        return out
+
+    def grayscale(self, packed: Optional[torch.Tensor] = None, size: int = 84, channels: int = 1,
+                  as_u8: bool = False) -> torch.Tensor:
+        """convert_grayscale(board, size) [+ _rgb] per env: [n][size][size][channels]."""
+        packed = self.obs if packed is None else packed
+        out = torch.empty((self.n, size, size, channels),
+                          dtype=torch.uint8 if as_u8 else torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            C.check(self._L.st_grayscale(self._ctx, _ptr(packed), size, channels, int(as_u8),
+                                         _ptr(out), self._stream()))
+        return out
+
+    # ------------------------------------------------------------ state
+    def _sizes(self):
+        W, sd = self.width, self.stride
+        return dict(board=(W, sd), piece=(sd,), stats=(C.NSTAT, sd), mt=(sd, C.MT_N))
+
+    def _view_ptr(self, name):
+        return getattr(self._views, name)
+
+    def state_tensors(self, fields=("board", "piece", "stats")) -> dict:
+        """Device copies of the state (full stride; slice [..., :n] for real envs)."""
+        out = {}
+        with torch.cuda.device(self.device):
+            for f in fields:
+                shape = self._sizes()[f]
+                t = torch.empty(shape, dtype=torch.int32, device=self.device)
+                C.check(self._L.st_copy(_ptr(t), ctypes.c_void_p(self._view_ptr(f)),
+                                        t.numel() * 4, self._stream()))
+                out[f] = t
+        return out
+
+    def get_state(self, fields=("board", "piece", "stats", "mt")) -> dict:
+        """Host (numpy, uint32/int32) copy of the state of the real envs."""
+        t = self.state_tensors(fields)
+        torch.cuda.synchronize(self.device)
+        out = {}
+        for f, v in t.items():
+            a = v.cpu().numpy()
+            if f in ("board", "piece", "mt"):
+                a = a.view(np.uint32)
+            out[f] = a[: self.n] if f == "mt" else a[..., : self.n]
+        return out
+
+    def set_state(self, **fields):
+        """Upload state arrays for the real envs (shapes as returned by
+        get_state); padding envs keep their current state."""
+        cur = self.state_tensors(tuple(fields))
+        with torch.cuda.device(self.device):
+            for f, v in fields.items():
+                full = cur[f].cpu().numpy().view(np.uint32).copy()
+                v = np.asarray(v).astype(np.int64).astype(np.uint32)
+                if f == "mt":
+                    full[: self.n] = v
+                else:
+                    full[..., : self.n] = v
+                t = torch.from_numpy(full.view(np.int32)).to(self.device)
+                C.check(self._L.st_copy(ctypes.c_void_p(self._view_ptr(f)), _ptr(t),
+                                        t.numel() * 4, self._stream()))
+            torch.cuda.synchronize(self.device)
+
+    def render_packed(self, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """TetrisEngine.render() (tetris_env.py:317-321): board + current piece,
+        packed u32 [W][n], without stepping."""
+        out = torch.empty((self.width, self.n), dtype=torch.int32, device=self.device) \
+            if out is None else out
+        with torch.cuda.device(self.device):
+            C.check(self._L.st_render(self._ctx, _ptr(out), self._stream()))
+        return out
+
+    def info_tensors(self) -> dict:
+        """get_info() (tetris_env.py:232-241) for every env as int32 device tensors."""
+        st = self.state_tensors(("stats",))["stats"][:, : self.n]
+        return dict(time=st[C.STAT["time"]], score=st[C.STAT["score"]],
+                    lines_cleared=st[C.STAT["lines"]], holes=st[C.STAT["holes"]],
+                    deaths=st[C.STAT["deaths"]], piece_height=st[C.STAT["piece_height"]],
+                    statistics=st[C.STAT["count0"]: C.STAT["count0"] + 7],
+                    ep_time=st[C.STAT["ep_time"]], ep_score=st[C.STAT["ep_score"]],
+                    ep_lines=st[C.STAT["ep_lines"]], ep_holes=st[C.STAT["ep_holes"]])
+
+    def gen_actions(self, t: int, seed: int, global_offset: int = 0,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Synthetic uniform actions splitmix64(seed ^ ((t<<32) ^ e)) % 7 on device."""
+        out = self._act if out is None else out
+        with torch.cuda.device(self.device):
+            C.check(self._L.st_gen_actions(_ptr(out), self.n, int(t), ctypes.c_uint64(seed),
+                                           int(global_offset), self._stream()))
+        return out

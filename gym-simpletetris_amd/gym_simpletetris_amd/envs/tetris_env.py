@@ -1,0 +1,316 @@
+"""Gym surface of SimpleTetris-v0 on the MI355X engine.
+
+TetrisEnv     -- the reference's single-env class (tetris_env.py:338-467):
+                 same constructor kwargs, spaces, step/reset/render/close,
+                 numpy float32 observations, the reference's reward *types*
+                 (int / np.int64 / float / np.float64, R18) and info dict.
+                 By default its pieces come from CPython's GLOBAL `random`
+                 exactly as the reference's do (tetris_env.py:187): the global
+                 MT19937 state is uploaded before and read back after every
+                 call, so a program that seeds `random` gets the reference's
+                 games bit-for-bit.
+TetrisVecEnv  -- the batched surface: N envs, torch tensors on the GPU,
+                 per-env CPython MT19937 streams random.seed(seed + e).
+Both run every game rule in the HIP kernels (engine.TetrisBatch); there is no
+CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import random
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .. import _lib as C
+from .. import spaces
+from ..engine import SHAPE_NAMES, TetrisBatch
+
+
+def _obs_space(obs_type, width, height, extend_dims):
+    """tetris_env.py:381-392."""
+    if obs_type == "ram":
+        shape = (width, height, 1) if extend_dims else (width, height)
+    elif obs_type == "grayscale":
+        shape = (84, 84, 1) if extend_dims else (84, 84)
+    elif obs_type == "rgb":
+        shape = (84, 84, 3)
+    else:
+        return None
+    return spaces.Box(0, 1, shape=shape, dtype=np.float32)
+
+
+class TetrisEnv:
+    metadata = {"render.modes": ["human", "rgb_array"], "render_fps": 8}  # :339
+
+    def __init__(self, width=10, height=20, obs_type="ram", extend_dims=False,
+                 render_mode="rgb_array", reward_step=False, penalise_height=False,
+                 penalise_height_increase=False, advanced_clears=False, high_scoring=False,
+                 penalise_holes=False, penalise_holes_increase=False, lock_delay=0,
+                 step_reset=False, *, device=None, rng: str = "global", seed: Optional[int] = None):
+        if rng not in ("global", "private"):
+            raise ValueError("rng must be 'global' (CPython's random, like the reference) or 'private'")
+        self.width = width
+        self.height = height
+        self.obs_type = obs_type
+        self.extend_dims = extend_dims
+        self.render_mode = render_mode
+        self.window_size = 512
+        self.engine = TetrisBatch(1, width=width, height=height, lock_delay=lock_delay,
+                                  step_reset=step_reset, reward_step=reward_step,
+                                  penalise_height=penalise_height,
+                                  penalise_height_increase=penalise_height_increase,
+                                  advanced_clears=advanced_clears, high_scoring=high_scoring,
+                                  penalise_holes=penalise_holes,
+                                  penalise_holes_increase=penalise_holes_increase,
+                                  autoreset="none", device=device)
+        self._rng_mode = rng
+        self.engine.seed([0 if seed is None else seed])
+        if rng == "global" and seed is not None:
+            random.seed(seed)
+        self._scoring = dict(advanced_clears=advanced_clears, penalise_height=penalise_height,
+                             penalise_height_increase=penalise_height_increase)
+        self.action_space = spaces.Discrete(7)           # :377
+        self.observation_space = _obs_space(obs_type, width, height, extend_dims)
+        self.window = None
+        self.clock = None
+        self._stats = None         # last downloaded counters (host int64 [NSTAT])
+        self._started = False
+        self._rng_sync_state = None
+        self._piece, self._piece_dirty = 0, True
+        dev = self.engine.device
+        self._d_act = torch.zeros(1, dtype=torch.uint8, device=dev)
+        self._h_stats = np.zeros((C.NSTAT, self.engine.stride), np.int32)
+        self._h_mt = np.zeros(C.MT_N, np.uint32)
+        self._h_idx = np.zeros(1, np.int32)
+
+    # ------------------------------------------------------------- RNG mirror
+    def seed(self, seed=None):
+        """Seed the piece RNG: random.seed(seed) in 'global' mode (what a user
+        of the reference does), the env's private MT19937 otherwise."""
+        if self._rng_mode == "global":
+            random.seed(seed)
+        else:
+            self.engine.seed([0 if seed is None else seed])
+        return [seed]
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.engine.device).cuda_stream)
+
+    def _push_rng(self):
+        if self._rng_mode != "global":
+            return
+        state = random.getstate()
+        if self._rng_sync_state is not None and state == self._rng_sync_state:
+            return
+        internal = state[1]
+        self._h_mt[:] = np.asarray(internal[:C.MT_N], dtype=np.uint32)
+        self._h_idx[0] = internal[C.MT_N]
+        v = self.engine._views
+        L = self.engine._L
+        s = self._stream()
+        C.check(L.st_copy(ctypes.c_void_p(v.mt), ctypes.c_void_p(self._h_mt.ctypes.data),
+                          C.MT_N * 4, s))
+        C.check(L.st_copy(ctypes.c_void_p(v.stats + C.STAT["mt_index"] * v.stride * 4),
+                          ctypes.c_void_p(self._h_idx.ctypes.data), 4, s))
+
+    def _pull(self, prev_idx=None):
+        """Download the counters; in 'global' mode write the env's MT state
+        back into CPython's random if this call drew pieces."""
+        v = self.engine._views
+        L = self.engine._L
+        s = self._stream()
+        C.check(L.st_copy(ctypes.c_void_p(self._h_stats.ctypes.data), ctypes.c_void_p(v.stats),
+                          self._h_stats.nbytes, s))
+        torch.cuda.current_stream(self.engine.device).synchronize()
+        st = self._h_stats[:, 0].astype(np.int64)
+        if self._rng_mode == "global":
+            idx = int(st[C.STAT["mt_index"]])
+            if prev_idx is None or idx != prev_idx or self._rng_sync_state is None:
+                C.check(L.st_copy(ctypes.c_void_p(self._h_mt.ctypes.data), ctypes.c_void_p(v.mt),
+                                  C.MT_N * 4, s))
+                torch.cuda.current_stream(self.engine.device).synchronize()
+                old = random.getstate()
+                random.setstate((old[0], tuple(int(w) for w in self._h_mt) + (idx,), old[2]))
+            self._rng_sync_state = random.getstate()
+        return st
+
+    # ------------------------------------------------------------- gym API
+    def _get_info(self, st):
+        """TetrisEngine.get_info (tetris_env.py:232-241)."""
+        pw = int(self.engine.get_state(("piece",))["piece"][0]) if self._piece_dirty else self._piece
+        self._piece, self._piece_dirty = pw, False
+        c0 = C.STAT["count0"]
+        return {"time": int(st[C.STAT["time"]]),
+                "current_piece": SHAPE_NAMES[pw & 7],
+                "score": int(st[C.STAT["score"]]),
+                "lines_cleared": int(st[C.STAT["lines"]]),
+                "holes": int(st[C.STAT["holes"]]),
+                "deaths": int(st[C.STAT["deaths"]]),
+                "statistics": {SHAPE_NAMES[i]: int(st[c0 + i]) for i in range(7)}}
+
+    def _observation(self, packed: torch.Tensor):
+        """TetrisEnv._observation (tetris_env.py:413-433) + float32 cast."""
+        if self.obs_type == "ram":
+            out = self.engine.obs_to_f32(packed)[0]
+            obs = out.cpu().numpy()
+            return obs.reshape(self.width, self.height, 1) if self.extend_dims else obs
+        g = self.engine.grayscale(packed, 84, 1 if self.obs_type == "grayscale" else 3)[0]
+        obs = g.cpu().numpy()
+        if self.obs_type == "grayscale":
+            return obs if self.extend_dims else obs.reshape(84, 84)
+        return obs
+
+    def _typed_reward(self, r: int, done: bool, prev, st):
+        """Reproduce the Python type the reference's reward ends up with (R18)."""
+        if done:
+            return int(r)
+        c0 = C.STAT["count0"]
+        locked = int(st[c0:c0 + 7].sum()) > int(prev[c0:c0 + 7].sum())
+        if not locked:
+            return int(r)
+        if self._scoring["advanced_clears"]:
+            hp = C.STAT["piece_height"]
+            if self._scoring["penalise_height"] or (
+                    self._scoring["penalise_height_increase"] and st[hp] > prev[hp]):
+                return np.float64(r)
+            return float(r)
+        return np.int64(r)
+
+    def step(self, action):
+        """TetrisEnv.step (tetris_env.py:397-403)."""
+        if not self._started:
+            raise AttributeError("step() before reset(): the reference fails at tetris_env.py:244")
+        if isinstance(action, (bool, np.bool_)) or not isinstance(action, (int, np.integer)) \
+                or not 0 <= int(action) < 7:
+            raise KeyError(action)  # value_action_map[action], tetris_env.py:245
+        prev = self._stats
+        self._push_rng()
+        self._d_act.fill_(int(action))
+        packed, rew, done = self.engine.step(self._d_act, obs="packed")
+        obs = self._observation(packed)
+        r = int(rew[0].item())
+        d = bool(done[0].item())
+        st = self._pull(int(prev[C.STAT["mt_index"]]))
+        self._stats = st
+        self._piece_dirty = True
+        return obs, self._typed_reward(r, d, prev, st), d, self._get_info(st)
+
+    def reset(self, return_info=False):
+        """TetrisEnv.reset (tetris_env.py:405-411): clear(); obs is the empty
+        board (clear() returns the board before the new piece is drawn)."""
+        self._push_rng()
+        self.engine.reset()
+        self._started = True
+        st = self._pull()
+        self._stats = st
+        self._piece_dirty = True
+        zeros = torch.zeros((self.width, 1), dtype=torch.int32, device=self.engine.device)
+        obs = self._observation(zeros)
+        return (obs, self._get_info(st)) if return_info else obs
+
+    def render(self, mode="human"):
+        """render('rgb_array'): 160x160x3 uint8 frame (tetris_env.py:458-462)."""
+        if mode == "rgb_array":
+            packed = self.engine.render_packed()
+            img = self.engine.grayscale(packed, 160, 3, as_u8=True)[0]
+            return img.cpu().numpy()
+        if mode == "human":
+            raise NotImplementedError("render('human') needs pygame; out of scope for the GPU engine")
+        raise NotImplementedError(mode)
+
+    def close(self):
+        """tetris_env.py:466-467."""
+        if getattr(self, "engine", None) is not None:
+            self.engine.close()
+            self.engine = None
+
+
+class VecInfo:
+    """Lazy get_info() for N envs: counters are read from the device state
+    only when a key is accessed (int32 tensors on the GPU)."""
+
+    def __init__(self, engine: TetrisBatch):
+        self._engine = engine
+        self._cache = None
+
+    def _load(self):
+        if self._cache is None:
+            self._cache = self._engine.info_tensors()
+        return self._cache
+
+    def __getitem__(self, k):
+        return self._load()[k]
+
+    def keys(self):
+        return self._load().keys()
+
+    def __contains__(self, k):
+        return k in self._load()
+
+
+class TetrisVecEnv:
+    """N SimpleTetris-v0 envs stepped together on one GPU.
+
+    step(actions) -> (obs, reward int32 [N], done bool [N], info)
+      obs: float32 [N, W, H] ('ram', '(...,1)' with extend_dims), or
+           [N, 84, 84(, 1|3)] for 'grayscale' / 'rgb', or the packed uint32
+           [W, N] words with obs_format='packed'.
+    With autoreset=True (default) envs that died are reset inside the same
+    kernel (TetrisEngine.clear); the returned obs of such an env is its
+    terminal observation (what the reference's step returned) and
+    info['ep_score'] / ['ep_lines'] / ['ep_time'] / ['ep_holes'] hold the
+    finished episode's counters.  Buffers are reused between steps.
+    """
+
+    def __init__(self, num_envs: int, width=10, height=20, obs_type="ram", extend_dims=False,
+                 reward_step=False, penalise_height=False, penalise_height_increase=False,
+                 advanced_clears=False, high_scoring=False, penalise_holes=False,
+                 penalise_holes_increase=False, lock_delay=0, step_reset=False, *,
+                 device=None, seed: int = 0, global_offset: int = 0, autoreset: bool = True,
+                 obs_format: str = "f32"):
+        if obs_format not in ("f32", "packed"):
+            raise ValueError("obs_format must be 'f32' or 'packed'")
+        self.num_envs = int(num_envs)
+        self.width, self.height = width, height
+        self.obs_type, self.extend_dims, self.obs_format = obs_type, extend_dims, obs_format
+        self.engine = TetrisBatch(self.num_envs, width=width, height=height,
+                                  lock_delay=lock_delay, step_reset=step_reset,
+                                  reward_step=reward_step, penalise_height=penalise_height,
+                                  penalise_height_increase=penalise_height_increase,
+                                  advanced_clears=advanced_clears, high_scoring=high_scoring,
+                                  penalise_holes=penalise_holes,
+                                  penalise_holes_increase=penalise_holes_increase,
+                                  autoreset="same_step" if autoreset else "none", device=device)
+        self.engine.seed([seed + global_offset + e for e in range(self.num_envs)])
+        self.single_action_space = spaces.Discrete(7)
+        self.single_observation_space = _obs_space(obs_type, width, height, extend_dims)
+        self.device = self.engine.device
+
+    def _obs(self, packed, f32):
+        if self.obs_format == "packed":
+            return packed
+        if self.obs_type == "ram":
+            o = f32 if f32 is not None else self.engine.obs_to_f32(packed)
+            return o.unsqueeze(-1) if self.extend_dims else o
+        ch = 1 if self.obs_type == "grayscale" else 3
+        g = self.engine.grayscale(packed, 84, ch)
+        return g if (self.obs_type == "rgb" or self.extend_dims) else g.squeeze(-1)
+
+    def reset(self):
+        self.engine.reset()
+        zeros = torch.zeros((self.width, self.num_envs), dtype=torch.int32, device=self.device)
+        if self.obs_format == "packed":
+            return zeros
+        return self._obs(zeros, torch.zeros((self.num_envs, self.width, self.height),
+                                            device=self.device) if self.obs_type == "ram" else None)
+
+    def step(self, actions):
+        want_f32 = self.obs_format == "f32" and self.obs_type == "ram"
+        out = self.engine.step(actions, obs="f32" if want_f32 else "packed")
+        f32 = out[0] if want_f32 else None
+        return self._obs(self.engine.obs, f32), out[1], out[2], VecInfo(self.engine)
+
+    def close(self):
+        self.engine.close()

@@ -1,0 +1,184 @@
+/*
+ * simpletetris.h -- C ABI of the MI355X batched SimpleTetris step engine.
+ *
+ * This is the drop-in boundary for gym-simpletetris' per-step hot path.  The
+ * reference has no FFI: its interface is the Python class
+ * TetrisEnv/TetrisEngine in /root/reference/gym_simpletetris/envs/tetris_env.py.
+ * Each entry point below names the reference method it replaces; the Python
+ * host package (gym-simpletetris_amd/gym_simpletetris_amd) binds these with
+ * ctypes and re-exposes the reference's Gym surface.
+ *
+ * Conventions
+ *  - All functions return ST_OK (0) or a negative st_status; the message of
+ *    the last failure on the calling thread is st_last_error().
+ *  - Pointers named d_* are DEVICE pointers on the context's device; the
+ *    caller owns them.  Context state (boards, pieces, counters, MT19937
+ *    states) is owned by the context and lives in HBM.
+ *  - Every call that takes a stream is asynchronous on that stream
+ *    (NULL = the device's null stream).  Calls on one context must be
+ *    serialised by the caller (the reference env is not thread-safe either,
+ *    tetris_env.py:187 uses the global `random`).
+ *  - Env e's piece RNG is CPython's MT19937 seeded with random.seed(seed[e]):
+ *    results equal the reference run under the per-env isolation protocol
+ *    (random.setstate/getstate around every reset/step of env e).
+ */
+#ifndef SIMPLETETRIS_H
+#define SIMPLETETRIS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ST_ABI_VERSION 1
+
+typedef struct st_ctx st_ctx;
+typedef void *st_stream; /* hipStream_t */
+
+typedef enum st_status {
+    ST_OK = 0,
+    ST_EINVAL = -1,  /* bad argument (reference: ValueError/KeyError) */
+    ST_ENOMEM = -2,  /* device allocation failed */
+    ST_EHIP = -3,    /* HIP runtime error */
+    ST_ESTATE = -4   /* call order violated (e.g. step before seed) */
+} st_status;
+
+/* Scoring / rule flags: TetrisEngine.__init__ kwargs, tetris_env.py:126-137. */
+enum st_flags {
+    ST_REWARD_STEP = 1u << 0,               /* reward_step              :256 */
+    ST_PENALISE_HEIGHT = 1u << 1,           /* penalise_height          :286 */
+    ST_PENALISE_HEIGHT_INCREASE = 1u << 2,  /* penalise_height_increase :288 */
+    ST_ADVANCED_CLEARS = 1u << 3,           /* advanced_clears          :266 */
+    ST_HIGH_SCORING = 1u << 4,              /* high_scoring             :270 */
+    ST_PENALISE_HOLES = 1u << 5,            /* penalise_holes           :294 */
+    ST_PENALISE_HOLES_INCREASE = 1u << 6,   /* penalise_holes_increase  :296 */
+    ST_STEP_RESET = 1u << 7                 /* step_reset               :248 */
+};
+
+/* What st_step does when an env dies (reference: the caller decides). */
+enum st_autoreset {
+    ST_AUTORESET_NONE = 0,     /* exact single-env semantics: state stays as the
+                                  reference leaves it after a death step (incl.
+                                  the R8 erase at tetris_env.py:303); caller
+                                  calls st_reset(mask) like `if done: reset()` */
+    ST_AUTORESET_SAME_STEP = 1 /* TetrisEngine.clear() runs inside the same
+                                  kernel; obs is the terminal obs, terminal
+                                  counters go to the ST_STAT_EP_* rows */
+};
+
+typedef struct st_config {
+    int32_t width;      /* 4..32   (TetrisEnv width=10,  tetris_env.py:344) */
+    int32_t height;     /* 4..28   (TetrisEnv height=20, tetris_env.py:345) */
+    int32_t lock_delay; /* 0..32766 (tetris_env.py:356; negative acts as 0, :175) */
+    uint32_t flags;     /* st_flags */
+    int32_t autoreset;  /* st_autoreset */
+} st_config;
+
+/* Per-env int32 counters, SoA rows of the stats block (TetrisEngine.get_info,
+ * tetris_env.py:232-241). */
+enum st_stat {
+    ST_STAT_TIME = 0,
+    ST_STAT_SCORE = 1,
+    ST_STAT_LINES = 2,
+    ST_STAT_HOLES = 3,
+    ST_STAT_PIECE_HEIGHT = 4,
+    ST_STAT_DEATHS = 5,
+    ST_STAT_COUNT0 = 6,   /* shape_counts T,J,L,Z,S,I,O: rows 6..12 */
+    ST_STAT_MT_INDEX = 13,/* MT19937 index (0..624) */
+    ST_STAT_EP_TIME = 14, /* terminal counters of the last finished episode */
+    ST_STAT_EP_SCORE = 15,/* (ST_AUTORESET_SAME_STEP only)                   */
+    ST_STAT_EP_LINES = 16,
+    ST_STAT_EP_HOLES = 17,
+    ST_NSTAT = 18
+};
+
+/* Device views of the context-owned state.  `stride` (>= n_envs, multiple of
+ * 64) separates SoA rows.
+ *   board  : uint32 [width][stride]  bit y of word (x, e) = board[x, y]
+ *            (the reference's board[x, y], tetris_env.py:140, one bit-packed
+ *            uint32 per board row x of the (width, height) array)
+ *   piece  : uint32 [stride]  id | rot<<3 | anchor_x<<5 | anchor_y<<11 | lock<<17
+ *            id in shape_names order T,J,L,Z,S,I,O (tetris_env.py:19);
+ *            rot = number of rotate_left (rotated(cclk=False)) mod 4
+ *   stats  : int32 [ST_NSTAT][stride]
+ *   mt     : uint32 [stride][624] MT19937 words per env                      */
+typedef struct st_state_views {
+    uint32_t *board;
+    uint32_t *piece;
+    int32_t *stats;
+    uint32_t *mt;
+    int64_t n_envs;
+    int64_t stride;
+    int32_t width, height;
+} st_state_views;
+
+/* ---- lifecycle: TetrisEnv.__init__ (tetris_env.py:343-392) ---------------- */
+int st_create(st_ctx **out, const st_config *cfg, int device, int64_t n_envs);
+int st_destroy(st_ctx *ctx);                     /* TetrisEnv.close, :466 */
+
+/* random.seed(seed[e]) for every env (host array of n_envs uint64 seeds).
+ * Also initialises counters as TetrisEngine.__init__ does (time = score = -1,
+ * :165-166).  Required before the first st_reset. */
+int st_seed(st_ctx *ctx, const uint64_t *seeds_host, st_stream stream);
+
+/* TetrisEngine.clear (tetris_env.py:306-315) on every env with d_mask[e] != 0
+ * (d_mask == NULL: all envs).  The reference's reset observation is the empty
+ * board (clear() returns the board before the piece is drawn), so no
+ * observation is produced here. */
+int st_reset(st_ctx *ctx, const uint8_t *d_mask, st_stream stream);
+
+/* TetrisEnv.step (tetris_env.py:397-403) / TetrisEngine.step (:243-304) on
+ * every env.  d_actions: uint8 [n_envs] in 0..6 (values >= 7 are rejected on
+ * the host side by the wrapper; the kernel treats them as idle).
+ * Outputs (any may be NULL):
+ *   d_obs    : uint32 [width][n_envs]  packed observation (board + current
+ *              piece overlay, :301-302), same bit layout as st_state_views.board
+ *   d_reward : int32 [n_envs]   (every reference reward is integer-valued)
+ *   d_done   : uint8 [n_envs]                                                 */
+int st_step(st_ctx *ctx, const uint8_t *d_actions, uint32_t *d_obs, int32_t *d_reward,
+            uint8_t *d_done, st_stream stream);
+
+/* Same as st_step but also writes the float32 observation the reference
+ * returns (np.array(state, float32), :400): d_obs_f32 float [n_envs][width][height],
+ * fused into the step kernel. */
+int st_step_f32(st_ctx *ctx, const uint8_t *d_actions, uint32_t *d_obs, float *d_obs_f32,
+                int32_t *d_reward, uint8_t *d_done, st_stream stream);
+
+/* Packed obs (uint32 [width][n_envs]) -> float32 [n_envs][width][height]
+ * (TetrisEnv._observation 'ram' + the float32 cast, :400 / :421-424). */
+int st_obs_to_f32(st_ctx *ctx, const uint32_t *d_obs, float *d_out, st_stream stream);
+
+/* TetrisEngine.render() (tetris_env.py:317-321): board with the current
+ * piece overlaid, packed like st_step's d_obs (uint32 [width][n_envs]), for
+ * every env, without stepping. */
+int st_render(st_ctx *ctx, uint32_t *d_obs, st_stream stream);
+
+/* Grayscale / RGB image of packed observations: convert_grayscale(board, size)
+ * (tetris_env.py:76-114) [+ convert_grayscale_rgb, :117-122], evaluated in
+ * closed form per pixel.  d_out: [n_envs][size][size][channels]
+ * (channels 1 or 3), float32 (as_u8 == 0: TetrisEnv obs, :426-433) or uint8
+ * (as_u8 != 0: render('rgb_array'), :458-462).  Values 0 / 128 / 190. */
+int st_grayscale(st_ctx *ctx, const uint32_t *d_obs, int32_t size, int32_t channels,
+                 int32_t as_u8, void *d_out, st_stream stream);
+
+/* Device views of the state (valid until st_destroy). */
+int st_state(st_ctx *ctx, st_state_views *out);
+
+/* hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, stream) -- moves state
+ * between the views above and caller buffers (save/load, crafted states). */
+int st_copy(void *dst, const void *src, int64_t bytes, st_stream stream);
+
+/* Synthetic action source used by the benchmark and the parity tests:
+ * d_out[e] = splitmix64(seed ^ ((t << 32) ^ (global_offset + e))) % 7. */
+int st_gen_actions(uint8_t *d_out, int64_t n, int64_t t, uint64_t seed,
+                   int64_t global_offset, st_stream stream);
+
+/* Message for the last failed call on this thread ("" if none). */
+const char *st_last_error(void);
+int st_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIMPLETETRIS_H */

@@ -1,0 +1,149 @@
+"""CPU-only tests: the C-ABI library loads and exports every symbol the public
+header declares (no compute calls), host-side logic (sharding, gather packing
+over gloo with world_size 2, spaces, make), and that the product path refuses
+to run without a GPU (no CPU fallback)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from replay import GOLDEN
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "simpletetris.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(st_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    from gym_simpletetris_amd import _lib
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    names = header_functions()
+    assert len(names) >= 12
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    assert set(names) == set(_lib.EXPORTS)
+
+
+def test_library_is_gfx950_code_object():
+    from gym_simpletetris_amd import _lib
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+    assert b"k_step" in data
+
+
+def test_no_cpu_fallback():
+    import gym_simpletetris_amd as G
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError, match="GPU"):
+        G.TetrisBatch(4)
+
+
+def test_make_ids():
+    import gym_simpletetris_amd as G
+    with pytest.raises(KeyError):
+        G.make("SimpleTetris-v1")
+
+
+def test_spaces_stand_ins():
+    from gym_simpletetris_amd import spaces
+    d = spaces.Discrete(7)
+    assert d.n == 7 and d.contains(3) and not d.contains(7)
+    b = spaces.Box(0, 1, shape=(10, 20), dtype=np.float32)
+    assert b.shape == (10, 20) and b.dtype == np.float32
+
+
+def test_shard_range_covers_exactly():
+    from gym_simpletetris_amd.distributed import shard_range
+    for n in (1, 7, 64, 65536 * 8, 1000003):
+        for world in (1, 2, 3, 4, 8):
+            if world > n:
+                continue
+            seen = 0
+            for r in range(world):
+                off, cnt = shard_range(n, world, r)
+                assert off == seen
+                seen += cnt
+            assert seen == n
+
+
+def test_grayscale_closed_form_matches_reference_images():
+    """The per-pixel formula st_grayscale evaluates (R19), restated in numpy,
+    equals convert_grayscale's output recorded from the reference."""
+    d = np.load(os.path.join(GOLDEN, "grayscale.npz"))
+    for i, (W, H) in enumerate(d["dims"]):
+        board = d["boards"][i][:W, :H]
+        for size, key in ((84, "g84"), (160, "g160")):
+            lim = max(W, H)
+            gap = size // 100 + 1
+            blk = (size - 2 * gap) // lim - gap
+            pitch = blk + gap
+            pr = (size - (gap + pitch * H)) // 2
+            pc = (size - (gap + pitch * W)) // 2
+            r = np.arange(size)[:, None] - pr
+            c = np.arange(size)[None, :] - pc
+            inside = (r >= 0) & (c >= 0) & (r < gap + pitch * H) & (c < gap + pitch * W)
+            cell = inside & (r % pitch >= gap) & (c % pitch >= gap)
+            y = np.clip(r // pitch, 0, H - 1)
+            x = np.clip(c // pitch, 0, W - 1)
+            img = np.where(inside, 128, 0)
+            img = np.where(cell & (board[x, y] != 0), 190, img)
+            assert np.array_equal(img, d[key][i]), (i, size)
+
+
+def _gather_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from gym_simpletetris_amd.distributed import (assemble, buffer_views, gather_outputs,
+                                                  output_buffer, shard_range)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    W, n_global = 10, 64
+    off, n = shard_range(n_global, world, rank)
+    buf = output_buffer(W, n, "cpu")
+    obs, rew, done = buffer_views(buf, W)
+    g = torch.arange(off, off + n, dtype=torch.int32)
+    obs[:] = g[None, :] * 16 + torch.arange(W, dtype=torch.int32)[:, None]
+    rew[:] = -g
+    done[:] = (g % 3 == 0).to(torch.uint8)
+    bufs = gather_outputs(buf)
+    if rank == 0:
+        o, r, d = assemble(bufs, W)
+        ok = (torch.equal(r, -torch.arange(n_global, dtype=torch.int32))
+              and torch.equal(d, (torch.arange(n_global) % 3 == 0).to(torch.uint8))
+              and torch.equal(o[3], torch.arange(n_global, dtype=torch.int32) * 16 + 3))
+        q.put(ok)
+    dist.destroy_process_group()
+
+
+def test_gather_packing_gloo_world2():
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=5) is True
+
+
+def test_algorithmic_bytes_formula():
+    import bench
+    b = bench.algorithmic_bytes(10, 20, 0.0, False)
+    assert b == (1 + 4 + 4 + 40) + (4 + 4 + 4 + 1 + 40)
+    assert bench.algorithmic_bytes(10, 20, 0.0, True) == b + 800
+    assert bench.algorithmic_bytes(10, 20, 1.0, False) > b

@@ -1,0 +1,298 @@
+"""HIP engine parity: the C-ABI library (libsimpletetris.so) on the GPU vs the
+reference's own outputs (tests/golden/*.npz) and the C oracle.  Bit-exact for
+every field (integer / bit work: no tolerance)."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from replay import GOLDEN, load_set, replay_crafted, replay_rollout
+
+pytestmark = pytest.mark.gpu
+
+ROLL = load_set("rollouts.npz")
+GREEDY = load_set("greedy.npz")
+CRAFTED = load_set("crafted.npz")
+
+
+def _engine():
+    import gym_simpletetris_amd as G
+    return G
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm device")
+
+
+class HipAdapter:
+    """TetrisBatch(autoreset='none') behind the replay interface."""
+
+    def __init__(self, n, seeds, kw):
+        G = _engine()
+        self.b = G.TetrisBatch(n, autoreset="none", seeds=seeds, **kw)
+        self.n = n
+
+    def reset(self, mask):
+        m = torch.as_tensor(np.asarray(mask, np.uint8), device=self.b.device)
+        self.b.reset(None if bool(np.all(mask)) else m)
+
+    def set_state(self, i, init):
+        st = self.b.get_state(("board", "piece", "stats"))
+        st["board"][:, i] = init["board"]
+        st["piece"][i] = init["piece"]
+        s = st["stats"]
+        s[0, i], s[1, i], s[2, i], s[3, i] = init["time"], init["score"], init["lines"], init["holes"]
+        s[4, i], s[5, i] = init["height"], init["deaths"]
+        s[6:13, i] = init["counts"]
+        self.b.set_state(**st)
+
+    def step(self, actions):
+        obs, rew, done = self.b.step(torch.as_tensor(np.asarray(actions, np.uint8),
+                                                     device=self.b.device), obs="packed")
+        st = self.b.get_state(("board", "piece", "stats"))
+        s = st["stats"]
+        return dict(reward=rew.cpu().numpy(), done=done.cpu().numpy().astype(np.uint8),
+                    time=s[0], score=s[1], lines=s[2], holes=s[3], height=s[4], deaths=s[5],
+                    counts=s[6:13].T, piece=st["piece"],
+                    obs=obs.cpu().numpy().view(np.uint32).T, board=st["board"].T)
+
+
+def test_library_is_the_hip_build():
+    G = _engine()
+    from gym_simpletetris_amd import _lib
+    L = _lib.load()
+    assert L.st_abi_version() == 1
+    b = G.TetrisBatch(3, seeds=[1, 2, 3])
+    b.reset()
+    b.step(np.zeros(3, np.uint8))
+    torch.cuda.synchronize()
+
+
+def test_device_mt19937_matches_cpython():
+    """Seed kernel (init_by_array + first twist) == CPython's first 624 outputs."""
+    G = _engine()
+    d = np.load(f"{GOLDEN}/mt19937.npz")
+    seeds = [int(s) for s in d["seeds"]]
+    b = G.TetrisBatch(len(seeds), seeds=seeds)
+    mt = b.get_state(("mt",))["mt"]
+
+    def temper(y):
+        y = y ^ (y >> np.uint32(11))
+        y = y ^ ((y << np.uint32(7)) & np.uint32(0x9D2C5680))
+        y = y ^ ((y << np.uint32(15)) & np.uint32(0xEFC60000))
+        return y ^ (y >> np.uint32(18))
+
+    for i in range(len(seeds)):
+        assert np.array_equal(temper(mt[i]), d["words"][i][:624]), f"seed {seeds[i]}"
+
+
+@pytest.mark.parametrize("name", sorted(CRAFTED))
+def test_hip_crafted(name):
+    meta, arrs = CRAFTED[name]
+    replay_crafted(HipAdapter, name, meta, arrs)
+
+
+@pytest.mark.parametrize("name", sorted(ROLL))
+def test_hip_uniform_rollouts(name):
+    meta, arrs = ROLL[name]
+    replay_rollout(HipAdapter, name, meta, arrs)
+
+
+@pytest.mark.parametrize("name", sorted(GREEDY))
+def test_hip_greedy_rollouts(name):
+    meta, arrs = GREEDY[name]
+    replay_rollout(HipAdapter, name, meta, arrs)
+
+
+def _oracle_vs_hip(n, steps, kw, seed_base=7, action_seed=99, autoreset="none"):
+    """Full-size bit-exact check against the C oracle on splitmix64 actions."""
+    G = _engine()
+    b = G.TetrisBatch(n, autoreset=autoreset, seeds=[seed_base + e for e in range(n)], **kw)
+    b.reset()
+    ob = O.OracleBatch(n, [seed_base + e for e in range(n)], **kw)
+    ob.reset()
+    acts = O.splitmix64_actions(action_seed, 0, steps, n)
+    ref = ob.rollout(acts)
+    for t in range(steps):
+        a = b.gen_actions(t, action_seed)
+        assert np.array_equal(a.cpu().numpy(), acts[t])
+        obs, rew, done = b.step(a, obs="packed")
+        assert np.array_equal(rew.cpu().numpy(), ref["reward"][t]), f"reward t={t}"
+        d = done.cpu().numpy()
+        assert np.array_equal(d.astype(np.uint8), ref["done"][t]), f"done t={t}"
+        assert np.array_equal(obs.cpu().numpy().view(np.uint32).T, ref["obs"][t]), f"obs t={t}"
+        if autoreset == "none" and d.any():
+            b.reset(torch.as_tensor(d.astype(np.uint8), device=b.device))
+    return ref
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(advanced_clears=True, penalise_holes_increase=True,
+                                             penalise_height_increase=True)])
+def test_hip_vs_oracle_full_size(kw):
+    """N = 65,536 (BASELINE configs C3/C4) bit-exact vs the oracle, 48 steps."""
+    _oracle_vs_hip(65536, 48, dict(width=10, height=20, **kw))
+
+
+def test_hip_vs_oracle_lock_delay_odd_board():
+    _oracle_vs_hip(4096, 120, dict(width=9, height=15, lock_delay=2, step_reset=True,
+                                   penalise_height=True, penalise_holes=True, reward_step=True))
+
+
+def test_same_step_autoreset_equals_explicit_reset():
+    """autoreset='same_step' == 'none' + reset(done) on the same stream."""
+    G = _engine()
+    n, T = 2048, 300
+    a = G.TetrisBatch(n, autoreset="none", seeds=range(n), penalise_holes_increase=True)
+    b = G.TetrisBatch(n, autoreset="same_step", seeds=range(n), penalise_holes_increase=True)
+    a.reset()
+    b.reset()
+    for t in range(T):
+        act = a.gen_actions(t, 5)
+        oa, ra, da = a.step(act)
+        oa, ra, da = oa.clone(), ra.clone(), da.clone()
+        ob, rb, db = b.step(act)
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
+        if da.any():
+            ia = a.info_tensors()
+            ib = b.info_tensors()
+            dd = da
+            assert torch.equal(ia["score"][dd], ib["ep_score"][dd])
+            assert torch.equal(ia["time"][dd], ib["ep_time"][dd])
+            assert torch.equal(ia["lines_cleared"][dd], ib["ep_lines"][dd])
+            a.reset(da.to(torch.uint8))
+    sa, sb = a.get_state(), b.get_state()
+    for k in ("board", "piece", "mt"):
+        assert np.array_equal(sa[k], sb[k]), k
+    assert np.array_equal(sa["stats"][:14], sb["stats"][:14])
+
+
+def test_sharding_invariance():
+    """Envs keyed by global index: one batch of N == two shards of N/2."""
+    G = _engine()
+    n, T, seed = 1000, 200, 31
+    full = G.TetrisBatch(n, autoreset="same_step", seeds=[seed + e for e in range(n)])
+    h = n // 2
+    sh = [G.TetrisBatch(h, autoreset="same_step", seeds=[seed + off + e for e in range(h)])
+          for off in (0, h)]
+    for b in [full] + sh:
+        b.reset()
+    for t in range(T):
+        of, rf, df = full.step(full.gen_actions(t, 77))
+        parts = [b.step(b.gen_actions(t, 77, global_offset=off))
+                 for b, off in zip(sh, (0, h))]
+        assert torch.equal(rf, torch.cat([p[1] for p in parts]))
+        assert torch.equal(df, torch.cat([p[2] for p in parts]))
+        assert torch.equal(of, torch.cat([p[0] for p in parts], dim=1))
+
+
+def test_fused_f32_obs_equals_unpacked():
+    G = _engine()
+    for (W, H, n) in [(10, 20, 1000), (7, 13, 333), (12, 26, 64)]:
+        b = G.TetrisBatch(n, width=W, height=H, seeds=range(n), autoreset="same_step")
+        b.reset()
+        for t in range(40):
+            f32, rew, done = b.step(b.gen_actions(t, 3), obs="f32")
+            ref = b.obs_to_f32(b.obs)
+            assert torch.equal(f32, ref), (W, H, t)
+            bits = ((b.obs.cpu().numpy().view(np.uint32).T[:, :, None] >> np.arange(H)) & 1)
+            assert np.array_equal(ref.cpu().numpy(), bits.astype(np.float32))
+
+
+def test_grayscale_kernel_matches_reference_images():
+    G = _engine()
+    d = np.load(f"{GOLDEN}/grayscale.npz")
+    for i, (W, H) in enumerate(d["dims"]):
+        if W < 4 or H < 4:
+            continue
+        b = G.TetrisBatch(1, width=int(W), height=int(H), seeds=[0])
+        cols = (d["boards"][i][:W, :H].astype(np.uint64) << np.arange(H, dtype=np.uint64)).sum(1)
+        packed = torch.as_tensor(cols.astype(np.uint32).view(np.int32)[:, None].copy(),
+                                 device=b.device)
+        for size, key in ((84, "g84"), (160, "g160")):
+            g = b.grayscale(packed, size, 1)[0, :, :, 0].cpu().numpy()
+            assert np.array_equal(g, d[key][i].astype(np.float32)), (i, size)
+            g3 = b.grayscale(packed, size, 3, as_u8=True)[0].cpu().numpy()
+            assert np.array_equal(g3, np.repeat(d[key][i][:, :, None], 3, axis=2)), (i, size)
+
+
+# ---------------------------------------------------------------- single-env surface
+@pytest.mark.parametrize("name", ["default", "adv_holes_height", "high_height_holes", "lock2_reset"])
+@pytest.mark.parametrize("rng", ["private", "global"])
+def test_single_env_surface_vs_reference(name, rng):
+    """TetrisEnv (reference surface): obs float32 arrays, reward values AND
+    Python types, done, info dict -- vs the reference's recorded env 0."""
+    G = _engine()
+    sets = GREEDY if name in GREEDY else ROLL
+    meta, arrs = sets[name]
+    kw = dict(meta["cfg"])
+    seed = meta["seed_base"]
+    env = G.TetrisEnv(rng=rng, seed=seed if rng == "private" else None, **kw)
+    if rng == "global":
+        random.seed(seed)
+    obs = env.reset()
+    assert obs.dtype == np.float32 and not obs.any()
+    W = kw.get("width", 10)
+    H = kw.get("height", 20)
+    types = {0: int, 1: np.int64, 2: float, 3: np.float64}
+    for t in range(min(300, arrs["actions"].shape[0])):
+        o, r, d, info = env.step(int(arrs["actions"][t, 0]))
+        assert o.shape == (W, H) and o.dtype == np.float32
+        bits = ((arrs["obs"][t, 0][:, None] >> np.arange(H)) & 1).astype(np.float32)
+        assert np.array_equal(o, bits), t
+        assert r == arrs["reward"][t, 0] and type(r) is types[int(arrs["rtype"][t, 0])], \
+            (t, r, type(r), arrs["rtype"][t, 0])
+        assert d == bool(arrs["done"][t, 0])
+        assert info["time"] == arrs["time"][t, 0] and info["score"] == arrs["score"][t, 0]
+        assert info["holes"] == arrs["holes"][t, 0] and info["deaths"] == arrs["deaths"][t, 0]
+        assert info["lines_cleared"] == arrs["lines"][t, 0]
+        assert list(info["statistics"].values()) == list(arrs["counts"][t, 0])
+        assert info["current_piece"] == G.SHAPE_NAMES[int(arrs["piece"][t, 0]) & 7]
+        if d:
+            env.reset()
+    if rng == "global":
+        # the global MT state must be where the reference leaves it
+        ob = O.OracleBatch(1, [seed], **kw)
+        ob.reset()
+        ob.rollout(arrs["actions"][:min(300, arrs["actions"].shape[0]), :1])
+        st = random.getstate()[1]
+        mt = np.ctypeslib.as_array(ob.envs[0].rng.mt)
+        assert np.array_equal(np.asarray(st[:624], np.uint32), mt)
+    env.close()
+
+
+def test_single_env_errors_and_render():
+    G = _engine()
+    env = G.make("SimpleTetris-v0", rng="private", seed=3)
+    with pytest.raises(AttributeError):
+        env.step(0)
+    env.reset()
+    with pytest.raises(KeyError):
+        env.step(7)
+    img = env.render("rgb_array")
+    assert img.shape == (160, 160, 3) and img.dtype == np.uint8
+    assert set(np.unique(img)) <= {0, 128, 190} and (img == 190).any()  # piece drawn
+    g = G.make("SimpleTetris-v0", obs_type="grayscale", extend_dims=True, rng="private")
+    o = g.reset()
+    assert o.shape == (84, 84, 1) and o.dtype == np.float32
+    o, r, d, info = g.step(2)
+    assert set(np.unique(o)) <= {0.0, 128.0, 190.0}
+    rgb = G.make("SimpleTetris-v0", obs_type="rgb", rng="private")
+    rgb.reset()
+    o, *_ = rgb.step(6)
+    assert o.shape == (84, 84, 3)
+
+
+def test_vec_env_surface():
+    G = _engine()
+    v = G.make("SimpleTetrisVec-v0", num_envs=256, seed=11, advanced_clears=True)
+    o = v.reset()
+    assert o.shape == (256, 10, 20) and o.dtype == torch.float32 and not o.any()
+    for t in range(100):
+        o, r, d, info = v.step(torch.randint(0, 7, (256,), dtype=torch.uint8, device=v.device))
+        assert o.shape == (256, 10, 20) and r.dtype == torch.int32 and d.dtype == torch.bool
+    assert info["time"].shape == (256,)
+    assert int(info["deaths"].sum()) > 0
