@@ -4,12 +4,15 @@
 // st_kernels.hip on the caller's stream.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "st_internal.h"
 
 struct st_ctx {
     st_config cfg;
+    uint32_t ablate;
+    uint64_t *stamps;
     int device;
     int64_t n;
     int64_t stride;
@@ -64,6 +67,8 @@ st::KParams params(const st_ctx *c) {
     p.lock_mod = (c->cfg.lock_delay > 0 ? c->cfg.lock_delay : 0) + 1;
     p.flags = c->cfg.flags;
     p.autoreset = c->cfg.autoreset;
+    p.ablate = c->ablate;
+    p.stamps = c->stamps;
     p.n = c->n;
     p.stride = c->stride;
     p.board = c->board;
@@ -78,6 +83,8 @@ void free_state(st_ctx *c) {
     if (c->piece) (void)hipFree(c->piece);
     if (c->stats) (void)hipFree(c->stats);
     if (c->mt) (void)hipFree(c->mt);
+    if (c->stamps) (void)hipFree(c->stamps);
+    c->stamps = nullptr;
     c->board = c->piece = c->mt = nullptr;
     c->stats = nullptr;
 }
@@ -112,6 +119,7 @@ int st_create(st_ctx **out, const st_config *cfg, int device, int64_t n_envs) {
     st_ctx *c = new st_ctx();
     c->cfg = *cfg;
     c->device = device;
+    if (const char *ab = getenv("ST_ABLATE")) c->ablate = (uint32_t)strtoul(ab, nullptr, 0);
     c->n = n_envs;
     c->stride = (n_envs + st::kWave - 1) / st::kWave * st::kWave;
     const size_t sd = (size_t)c->stride;
@@ -120,6 +128,8 @@ int st_create(st_ctx **out, const st_config *cfg, int device, int64_t n_envs) {
     if (e == hipSuccess) e = hipMalloc(&c->piece, sd * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&c->stats, sd * ST_NSTAT * sizeof(int32_t));
     if (e == hipSuccess) e = hipMalloc(&c->mt, sd * st::kMtN * sizeof(uint32_t));
+    if (e == hipSuccess && getenv("ST_STAMPS"))
+        e = hipMalloc(&c->stamps, (sd / st::kWave) * 8 * sizeof(uint64_t));
     if (e != hipSuccess) {
         free_state(c);
         delete c;
@@ -245,6 +255,17 @@ int st_state(st_ctx *c, st_state_views *out) {
     out->stride = c->stride;
     out->width = c->cfg.width;
     out->height = c->cfg.height;
+    return ST_OK;
+}
+
+int st_debug_stamps(st_ctx *c, uint64_t *host_out, int64_t max_words) {
+    if (!c || !host_out) return fail(ST_EINVAL, "st_debug_stamps: null argument");
+    if (!c->stamps) return fail(ST_ESTATE, "context was not created with ST_STAMPS set");
+    DeviceGuard g(c->device);
+    int64_t n = (c->stride / st::kWave) * 8;
+    if (max_words < n) n = max_words;
+    ST_HIP(hipDeviceSynchronize());
+    ST_HIP(hipMemcpy(host_out, c->stamps, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return ST_OK;
 }
 

@@ -12,12 +12,21 @@ constexpr int kPad = 4;        // wall columns on each side of the LDS board
 constexpr int kMaxW = 32;
 constexpr int kMaxH = 28;
 constexpr int kMtN = 624;
+constexpr int kStatRows = 14;                // stats rows 0..13 move with every step
+constexpr int kPieceRow = kStatRows;         // staged row 14 = piece word
+constexpr int kHotRows = kStatRows + 1;
+constexpr int kHotQ = (kHotRows * 16 + kWave - 1) / kWave;  // 16-B slots per lane
 
 struct KParams {
     int32_t W, H;
     int32_t lock_mod;   // max(lock_delay, 0) + 1   (tetris_env.py:175)
     uint32_t flags;
     int32_t autoreset;
+    uint32_t ablate;    // TIMING DIAGNOSTICS ONLY (env ST_ABLATE at st_create); 0 in
+                        // every correct run: 1 = no lock path, 2 = no MT draw,
+                        // 4 = no twist, 8 = no obs output
+    uint64_t *stamps;   // DIAGNOSTIC build only (env ST_STAMPS at st_create): per-wave
+                        // s_memtime at 8 phase boundaries of the step kernel
     int64_t n;          // real envs
     int64_t stride;     // padded env count (multiple of 64) = SoA row stride
     // state

@@ -85,6 +85,15 @@ __constant__ uint32_t c_tab[28] = {
     kTab.d[14], kTab.d[15], kTab.d[16], kTab.d[17], kTab.d[18], kTab.d[19], kTab.d[20],
     kTab.d[21], kTab.d[22], kTab.d[23], kTab.d[24], kTab.d[25], kTab.d[26], kTab.d[27]};
 
+// Piece table entry `lane` (lanes 0..27) materialised from immediates: no
+// memory round trip at kernel entry.
+__device__ __forceinline__ uint32_t tab_entry(int lane) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 28; ++j) v = lane == j ? kTab.d[j] : v;
+    return v;
+}
+
 __device__ __forceinline__ int col_dx(uint32_t c) { return (int)(c & 7u) - 3; }
 __device__ __forceinline__ int col_top(uint32_t c) { return (int)((c >> 3) & 7u) - 3; }
 __device__ __forceinline__ int col_bot(uint32_t c) { return col_top(c) + (int)(c >> 6); }
@@ -101,32 +110,38 @@ __device__ __forceinline__ uint32_t &lcol(uint32_t *L, int x, int lane) {
     return L[(x + kPad) * kWave + lane];
 }
 
-// is_occupied (tetris_env.py:29-36) for piece descriptor `d` at anchor (x, y).
-__device__ __forceinline__ bool collides(uint32_t *L, int lane, uint32_t d, int x, int y) {
-    uint32_t hit = 0;
+// The four column words a descriptor touches at anchor column x (issued as
+// one batch of LDS reads), and the collision / drop tests on them:
+//  collides_v = is_occupied (tetris_env.py:29-36) with the floor bits and the
+//    all-ones wall columns standing in for the bounds checks; cells with y < 0
+//    vanish in run_bits (R2);
+//  drop_v = the number of free soft_drops below a legal position, i.e.
+//    hard_drop's loop count (tetris_env.py:54-59): only each column's lowest
+//    cell can meet an obstacle first, and the first obstacle row is the lowest
+//    set bit of (column | floor) at or below it.  A column outside the board
+//    (legal only while its cells are above row 0) reads a wall and stops the
+//    piece as its lowest cell would enter row 0.
+__device__ __forceinline__ void read_cols(const uint32_t *L, int lane, uint32_t d, int x,
+                                          uint32_t (&v)[4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const uint32_t c = (d >> (8 * j)) & 0xFFu;
-        hit |= run_bits(c, y) & lcol(L, x + col_dx(c), lane);
+        v[j] = L[(x + col_dx(c) + kPad) * kWave + lane];
     }
+}
+__device__ __forceinline__ bool collides_v(uint32_t d, int y, const uint32_t (&v)[4]) {
+    uint32_t hit = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) hit |= run_bits((d >> (8 * j)) & 0xFFu, y) & v[j];
     return hit != 0;
 }
-
-// Number of free soft_drops below a legal position: hard_drop's loop count
-// (tetris_env.py:54-59).  Only each column's lowest cell can meet an obstacle
-// first; the first obstacle row is the lowest set bit of (column | floor)
-// at or below that cell.  Wall columns are all-ones, so a column that is
-// outside the board (legal only while its cells are above row 0) stops the
-// piece as its lowest cell would enter row 0 (R2).
-__device__ __forceinline__ int drop_distance(uint32_t *L, int lane, uint32_t d, int x, int y) {
+__device__ __forceinline__ int drop_v(uint32_t d, int y, const uint32_t (&v)[4]) {
     int dist = 1 << 20;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const uint32_t c = (d >> (8 * j)) & 0xFFu;
-        const int yb = y + col_bot(c);
+        const int yb = y + col_bot((d >> (8 * j)) & 0xFFu);
         const int s = yb + 1 > 0 ? yb + 1 : 0;
-        const uint32_t v = lcol(L, x + col_dx(c), lane) & (~0u << s);
-        const int k = __builtin_ctz(v) - yb - 1;
+        const int k = __builtin_ctz(v[j] & (~0u << s)) - yb - 1;
         dist = k < dist ? k : dist;
     }
     return dist;
@@ -137,7 +152,7 @@ __device__ __forceinline__ void paint(uint32_t *L, int lane, uint32_t d, int x, 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const uint32_t c = (d >> (8 * j)) & 0xFFu;
-        lcol(L, x + col_dx(c), lane) |= run_bits(c, y) & hmask;
+        atomicOr(&lcol(L, x + col_dx(c), lane), run_bits(c, y) & hmask);  // ds_or_b32
     }
 }
 
@@ -146,7 +161,7 @@ __device__ __forceinline__ void erase(uint32_t *L, int lane, uint32_t d, int x, 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const uint32_t c = (d >> (8 * j)) & 0xFFu;
-        lcol(L, x + col_dx(c), lane) &= ~(run_bits(c, y) & hmask);
+        atomicAnd(&lcol(L, x + col_dx(c), lane), ~(run_bits(c, y) & hmask));  // ds_and_b32
     }
 }
 
@@ -187,7 +202,19 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
 // chunks whose elements only read OLD words or words of earlier chunks:
 // [0,227) old | [227,454) uses [0,227) | [454,623) uses [227,396) | 623.
 __device__ void coop_twist(uint32_t *g, uint32_t *S, int lane) {
-    for (int i = lane; i < kMtN; i += kWave) S[i] = g[i];
+    {
+        uint32_t t[10];  // 624 = 9 * 64 + 48: issue all ten loads before any wait
+#pragma unroll
+        for (int q = 0; q < 10; ++q) {
+            const int i = lane + kWave * q;
+            t[q] = i < kMtN ? g[i] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 10; ++q) {
+            const int i = lane + kWave * q;
+            if (i < kMtN) S[i] = t[q];
+        }
+    }
     __syncthreads();
     uint32_t v[4];
 #pragma unroll
@@ -237,8 +264,19 @@ __device__ void coop_twist(uint32_t *g, uint32_t *S, int lane) {
 // Wave-uniform: every lane of the wave must call it.  Each round reads up to 8
 // consecutive words per lane (one or two 64-B lines of the env's MT block);
 // lanes whose state is exhausted are twisted cooperatively first.
-__device__ int draw_shape(bool need, int32_t (&cnt)[7], int32_t &mtidx, uint32_t *mt_wave,
-                          uint32_t *S, int lane) {
+// Issue the loads of the next 8 MT words of this lane's stream (used by the
+// step kernel as soon as it knows the lane locks, so the round trip overlaps
+// the lock-path work).
+__device__ __forceinline__ void prefetch_words(const uint32_t *g, int32_t mtidx, bool want,
+                                               uint32_t (&w)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        w[j] = (want && mtidx + j < kMtN) ? __builtin_nontemporal_load(g + mtidx + j) : 0u;
+}
+
+__device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], int32_t &mtidx,
+                                          uint32_t *mt_wave, uint32_t *S, int lane, bool twist,
+                                          const uint32_t (&pre)[8], bool have_pre) {
     int32_t maxc = cnt[0], sumc = cnt[0];
 #pragma unroll
     for (int i = 1; i < 7; ++i) {
@@ -249,24 +287,46 @@ __device__ int draw_shape(bool need, int32_t (&cnt)[7], int32_t &mtidx, uint32_t
     const int k = 32 - __builtin_clz(n);
     uint32_t *g = mt_wave + (size_t)lane * kMtN;
     bool pending = need;
+    bool fresh = false;  // state twisted (and stored) by this wave in this launch
     uint32_t r = 0;
     while (__ballot(pending)) {
+        if (!twist && pending && mtidx >= kMtN) mtidx = 0;  // ablation: skip the twist
         uint64_t tw = __ballot(pending && mtidx >= kMtN);
+        uint32_t w[8];
+        bool have = false;
+        if (have_pre && pending && mtidx < kMtN) {  // words prefetched by the caller
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w[j] = pre[j];
+            have = true;
+        }
+        have_pre = false;
         if (tw) {
             do {
                 const int l = __builtin_ctzll(tw);
                 tw &= tw - 1;
                 coop_twist(mt_wave + (size_t)l * kMtN, S, lane);
+                if (lane == l) {  // the twisted lane takes its first words from LDS
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) w[j] = S[j];
+                    have = true;
+                }
+                __syncthreads();  // S is reused by the next lane's twist
             } while (tw);
-            // our own stores must land in L2 before the (L1-bypassing) reloads
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (pending && mtidx >= kMtN) mtidx = 0;
+            if (have) {
+                mtidx = 0;
+                fresh = true;
+            }
         }
-        if (pending) {
-            uint32_t w[8];
+        if (pending && !have) {
+            // A state twisted in this launch is re-read from global memory only
+            // if one draw needs more than 8 of its words (p ~ 1e-3): drain our
+            // stores to L2 first; the nt loads bypass the (stale) L1.
+            if (__ballot(pending && fresh)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
             for (int j = 0; j < 8; ++j)
                 w[j] = (mtidx + j < kMtN) ? __builtin_nontemporal_load(g + mtidx + j) : 0u;
+        }
+        if (pending) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 if (pending && mtidx < kMtN) {
@@ -303,12 +363,27 @@ __device__ __forceinline__ uint32_t pack_piece(int id, int rot, int ax, int ay, 
 }
 
 // ---------------------------------------------------------------- step
-template <int WT, int HT, bool F32>
+// In-kernel phase stamps (diagnostic instantiation only; MI355X guide §7).
+#define ST_STAMP(i)                                                    \
+    do {                                                               \
+        if constexpr (STAMP) {                                         \
+            __builtin_amdgcn_sched_barrier(0);                         \
+            tstamp[i] = __builtin_amdgcn_s_memtime();                  \
+            __builtin_amdgcn_sched_barrier(0);                         \
+        }                                                              \
+    } while (0)
+
+template <int WT, int HT, bool F32, bool STAMP = false>
 __global__ __launch_bounds__(kWave) void k_step(KParams p) {
-    __shared__ uint32_t L[(kMaxW + 2 * kPad) * kWave];
+    [[maybe_unused]] uint64_t tstamp[8] = {};
+    ST_STAMP(0);
+    // LDS: board columns L[x + kPad][lane] (walls at both ends), the staged
+    // counter rows SS[r][lane] (r < 14: stats rows, 14: piece word), the MT
+    // twist scratch and the piece table.
+    __shared__ __attribute__((aligned(16))) uint32_t L[(kMaxW + 2 * kPad) * kWave];
+    __shared__ __attribute__((aligned(16))) uint32_t SS[kHotQ * 4 * kWave];
     __shared__ uint32_t S[kMtN];
     __shared__ uint32_t T[28];
-    __shared__ uint32_t O[F32 ? kWave * (kMaxW + 1) : 1];
     const int W = WT ? WT : p.W;
     const int H = HT ? HT : p.H;
     const int lane = threadIdx.x;
@@ -318,50 +393,83 @@ __global__ __launch_bounds__(kWave) void k_step(KParams p) {
     const bool real = e < p.n;
     const uint32_t hmask = (1u << H) - 1u;
     const uint32_t floorb = ~hmask;
-    if (lane < 28) T[lane] = c_tab[lane];
 
-    // ---- every load of the step, issued up front ----
+    // ---- loads: 16 B per lane (a wave's slice of one SoA row is 256 B) ----
+    // Unconditional (clamped) so the compiler issues them all back to back:
+    // board slots past the last column land in the right-wall columns, which
+    // are written after them; counter slots past row 14 land in padding row 15.
+    constexpr int NBQ = ((WT ? WT : kMaxW) * 16 + kWave - 1) / kWave;  // board x4 slots
+    uint4 bv[NBQ];
+#pragma unroll
+    for (int q = 0; q < NBQ; ++q) {
+        const int i = q * kWave + lane, c = i & 15;
+        const int x = (i >> 4) < W ? (i >> 4) : W - 1;
+        bv[q] = *reinterpret_cast<const uint4 *>(p.board + x * sd + e0 + 4 * c);
+    }
+    uint4 sv[kHotQ];
+#pragma unroll
+    for (int q = 0; q < kHotQ; ++q) {
+        const int i = q * kWave + lane, c = i & 15;
+        const int r = (i >> 4) < kHotRows ? (i >> 4) : kHotRows - 1;
+        const uint32_t *row = r < kStatRows ? reinterpret_cast<const uint32_t *>(p.stats) + r * sd
+                                            : p.piece;
+        sv[q] = *reinterpret_cast<const uint4 *>(row + e0 + 4 * c);
+    }
     const uint32_t act = real ? (uint32_t)p.actions[e] : 6u;
-    const uint32_t pw = p.piece[e];
-    int32_t *st = p.stats + e;
-    int32_t time = st[ST_STAT_TIME * sd];
-    int32_t score = st[ST_STAT_SCORE * sd];
-    int32_t lines = st[ST_STAT_LINES * sd];
-    int32_t holes = st[ST_STAT_HOLES * sd];
-    int32_t height = st[ST_STAT_PIECE_HEIGHT * sd];
-    int32_t deaths = st[ST_STAT_DEATHS * sd];
-    int32_t mtidx = st[ST_STAT_MT_INDEX * sd];
-    int32_t cnt[7];
+    if (lane < 28) T[lane] = tab_entry(lane);
 #pragma unroll
-    for (int i = 0; i < 7; ++i) cnt[i] = st[(ST_STAT_COUNT0 + i) * sd];
-#pragma unroll 8
-    for (int x = 0; x < W; ++x) lcol(L, x, lane) = p.board[x * sd + e] | floorb;
+    for (int q = 0; q < NBQ; ++q) {
+        const int i = q * kWave + lane, x = i >> 4, c = i & 15;
+        uint4 v = bv[q];
+        v.x |= floorb;
+        v.y |= floorb;
+        v.z |= floorb;
+        v.w |= floorb;
+        *reinterpret_cast<uint4 *>(&L[(x + kPad) * kWave + 4 * c]) = v;
+    }
 #pragma unroll
-    for (int x = 0; x < kPad; ++x) {
+    for (int x = 0; x < kPad; ++x) {  // walls (after the board slots, see above)
         L[x * kWave + lane] = ~0u;
         L[(W + kPad + x) * kWave + lane] = ~0u;
     }
-    __syncthreads();  // piece table visible to the wave
+#pragma unroll
+    for (int q = 0; q < kHotQ; ++q) {
+        const int i = q * kWave + lane, c = i & 15;
+        *reinterpret_cast<uint4 *>(&SS[(i >> 4) * kWave + 4 * c]) = sv[q];
+    }
+    __syncthreads();
+    auto ss = [&](int r) -> uint32_t & { return SS[r * kWave + lane]; };
 
+    const uint32_t pw = ss(kPieceRow);
+    int32_t time = (int32_t)ss(ST_STAT_TIME);
     const int id = (int)(pw & 7u);
     int rot = (int)((pw >> 3) & 3u);
     int ax = (int)((pw >> 5) & 63u);
     int ay = (int)((pw >> 11) & 63u);
     int lock = (int)(pw >> 17);
-    uint32_t desc = T[id * 4 + rot];
+    if constexpr (STAMP) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    ST_STAMP(1);
 
-    // ---- action (tetris_env.py:245; value_action_map :152-160) ----
-    if (act == 0u || act == 1u || act == 4u || act == 5u) {
-        const int cx = ax + (act == 0u ? -1 : (act == 1u ? 1 : 0));
-        const int cr = act == 4u ? ((rot + 1) & 3) : (act == 5u ? ((rot + 3) & 3) : rot);
-        const uint32_t cd = T[id * 4 + cr];
-        if (!collides(L, lane, cd, cx, ay)) {
-            ax = cx;
-            rot = cr;
-            desc = cd;
-        }
+    // ---- action (tetris_env.py:245; value_action_map :152-160) + drop ----
+    // Current and candidate descriptors and their columns are read in one
+    // LDS round trip each; the collision and drop tests are then pure VALU.
+    const bool tries = act == 0u || act == 1u || act == 4u || act == 5u;
+    const int cx = ax + (act == 0u ? -1 : (act == 1u ? 1 : 0));
+    const int cr = act == 4u ? ((rot + 1) & 3) : (act == 5u ? ((rot + 3) & 3) : rot);
+    uint32_t desc = T[id * 4 + rot];
+    const uint32_t cdesc = T[id * 4 + cr];
+    uint32_t cur[4], cand[4];
+    read_cols(L, lane, desc, ax, cur);
+    read_cols(L, lane, cdesc, cx, cand);
+    int d;
+    if (tries && !collides_v(cdesc, ay, cand)) {
+        ax = cx;
+        rot = cr;
+        desc = cdesc;
+        d = drop_v(cdesc, ay, cand);
+    } else {
+        d = drop_v(desc, ay, cur);
     }
-    int d = drop_distance(L, lane, desc, ax, ay);
     if (act == 2u) {                 // hard_drop :54-59
         ay += d;
         d = 0;
@@ -379,13 +487,26 @@ __global__ __launch_bounds__(kWave) void k_step(KParams p) {
     int32_t rew = (p.flags & ST_REWARD_STEP) ? 1 : 0;
     bool locknow = false;
     if (d == 0) {
-        lock = (lock + 1) % p.lock_mod;
-        locknow = lock == 0;
+        lock = lock + 1 < p.lock_mod ? lock + 1 : (p.lock_mod == 1 ? 0 : (lock + 1) % p.lock_mod);
+        locknow = lock == 0 && !(p.ablate & 1u);
     }
+    ST_STAMP(2);
+    // MT words for the piece this lock will draw: issue now, consume after the
+    // lock path (every locking lane draws: a spawn, or the same-step reset's).
+    int32_t mtidx = (int32_t)ss(ST_STAT_MT_INDEX);
+    uint32_t pre[8];
+    const bool want_pre = locknow && mtidx < kMtN && !(p.ablate & 2u);
+    prefetch_words(p.mt + e * kMtN, mtidx, want_pre, pre);
 
     // ---- lock path (tetris_env.py:263-299) ----
     bool died = false, spawn = false;
+    int32_t score = 0, lines = 0, holes = 0, height = 0, deaths = 0;
     if (locknow) {
+        score = (int32_t)ss(ST_STAT_SCORE);
+        lines = (int32_t)ss(ST_STAT_LINES);
+        holes = (int32_t)ss(ST_STAT_HOLES);
+        height = (int32_t)ss(ST_STAT_PIECE_HEIGHT);
+        deaths = (int32_t)ss(ST_STAT_DEATHS);
         paint(L, lane, desc, ax, ay, hmask);
         uint32_t andv = hmask, orv = 0;
         int32_t nh = 0;
@@ -441,67 +562,85 @@ __global__ __launch_bounds__(kWave) void k_step(KParams p) {
             spawn = true;
         }
     }
+    ST_STAMP(3);
 
     // ---- spawn (:299 _new_piece) or same-step reset (:306-315) ----
     const bool reset_now = died && p.autoreset == ST_AUTORESET_SAME_STEP;
-    const int pick = draw_shape(spawn || reset_now, cnt, mtidx, p.mt + e0 * kMtN, S, lane);
+    const bool draw = spawn || reset_now;
+    int32_t cnt[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) cnt[i] = draw ? (int32_t)ss(ST_STAT_COUNT0 + i) : 0;
+    const int pick = (p.ablate & 2u) ? 0
+                                      : draw_shape(draw, cnt, mtidx, p.mt + e0 * kMtN, S, lane,
+                                                   !(p.ablate & 4u), pre, want_pre);
+    ST_STAMP(4);
     uint32_t odesc = desc;
     int oax = ax, oay = ay;
     uint32_t pw_out = pack_piece(id, rot, ax, ay, lock);
-    if (spawn || reset_now) pw_out = pack_piece(pick, 0, W / 2, 0, lock);
+    if (draw) pw_out = pack_piece(pick, 0, W / 2, 0, lock);
     if (spawn) {
         odesc = T[pick * 4];
         oax = W / 2;
         oay = 0;
     }
-    if (died && !reset_now) erase(L, lane, desc, ax, ay, hmask);  // R8, :303
 
-    // ---- state + observation (tetris_env.py:301-304) ----
-#pragma unroll 8
-    for (int x = 0; x < W; ++x) {
-        if (locknow) p.board[x * sd + e] = reset_now ? 0u : (lcol(L, x, lane) & hmask);
-    }
-    paint(L, lane, odesc, oax, oay, hmask);
-#pragma unroll 8
-    for (int x = 0; x < W; ++x) {
-        const uint32_t v = lcol(L, x, lane) & hmask;
-        if (real && p.obs) p.obs[x * p.n + e] = v;
-        if (F32) O[lane * (W + 1) + x] = v;
-    }
-    p.piece[e] = pw_out;
+    // ---- counters back to the staged rows (tetris_env.py:253, :264-299) ----
     if (reset_now) {
+        int32_t *st = p.stats + e;
         st[ST_STAT_EP_TIME * sd] = time;
         st[ST_STAT_EP_SCORE * sd] = score;
         st[ST_STAT_EP_LINES * sd] = lines;
         st[ST_STAT_EP_HOLES * sd] = holes;
         time = score = lines = holes = height = 0;
     }
-    st[ST_STAT_TIME * sd] = time;
+    ss(ST_STAT_TIME) = (uint32_t)time;
+    ss(kPieceRow) = pw_out;
     if (locknow) {
-        st[ST_STAT_SCORE * sd] = score;
-        st[ST_STAT_LINES * sd] = lines;
-        st[ST_STAT_HOLES * sd] = holes;
-        st[ST_STAT_PIECE_HEIGHT * sd] = height;
-        st[ST_STAT_DEATHS * sd] = deaths;
-        st[ST_STAT_MT_INDEX * sd] = mtidx;
+        ss(ST_STAT_SCORE) = (uint32_t)score;
+        ss(ST_STAT_LINES) = (uint32_t)lines;
+        ss(ST_STAT_HOLES) = (uint32_t)holes;
+        ss(ST_STAT_PIECE_HEIGHT) = (uint32_t)height;
+        ss(ST_STAT_DEATHS) = (uint32_t)deaths;
+        ss(ST_STAT_MT_INDEX) = (uint32_t)mtidx;
+        if (draw) ss(ST_STAT_COUNT0 + pick) += 1u;  // shape_counts[name] += 1, :199
+    }
+
+    // ---- observation (tetris_env.py:301-302): board + current piece ----
+    paint(L, lane, odesc, oax, oay, hmask);
+    __syncthreads();
+    const bool wide_obs = (p.n & 3) == 0 && e0 + kWave <= p.n &&
+                          (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0;
+    if (p.obs && !(p.ablate & 8u)) {
+        if (wide_obs) {
 #pragma unroll
-        for (int i = 0; i < 7; ++i) st[(ST_STAT_COUNT0 + i) * sd] = cnt[i];
+            for (int q = 0; q < NBQ; ++q) {
+                const int i = q * kWave + lane, x = i >> 4, c = i & 15;
+                if (x < W) {
+                    uint4 v = *reinterpret_cast<const uint4 *>(&L[(x + kPad) * kWave + 4 * c]);
+                    v.x &= hmask;
+                    v.y &= hmask;
+                    v.z &= hmask;
+                    v.w &= hmask;
+                    *reinterpret_cast<uint4 *>(p.obs + x * p.n + e0 + 4 * c) = v;
+                }
+            }
+        } else if (real) {
+            for (int x = 0; x < W; ++x) p.obs[x * p.n + e] = lcol(L, x, lane) & hmask;
+        }
     }
     if (real) {
         if (p.reward) p.reward[e] = rew;
         if (p.done) p.done[e] = died ? 1 : 0;
     }
-
     if (F32) {
-        // float32 obs [n][W][H] for the wave's envs is one contiguous block:
-        // write it as 16-B chunks, lane-consecutive, reading the packed words
-        // back through LDS (row stride W+1 keeps the staging conflict-free).
-        __syncthreads();
+        // float32 obs [n][W][H] of the wave's envs is one contiguous block:
+        // 16-B chunks, lane-consecutive, bits read back from L.
         const int64_t nreal64 = p.n - e0 < kWave ? p.n - e0 : kWave;
         const int nreal = (int)nreal64;
         const int per_env = W * H;
         const int total = nreal * per_env;
         float *out = p.obs_f32 + e0 * per_env;
+        auto word = [&](int ee, int x) { return L[(x + kPad) * kWave + ee] & hmask; };
         if ((per_env & 3) == 0) {
             float4 *out4 = reinterpret_cast<float4 *>(out);
             for (int c = lane; c < total / 4; c += kWave) {
@@ -512,7 +651,7 @@ __global__ __launch_bounds__(kWave) void k_step(KParams p) {
                 const int y = rem - x * H;
                 float4 v;
                 if (y + 4 <= H) {
-                    const uint32_t w = O[ee * (W + 1) + x] >> y;
+                    const uint32_t w = word(ee, x) >> y;
                     v.x = (float)(w & 1u);
                     v.y = (float)((w >> 1) & 1u);
                     v.z = (float)((w >> 2) & 1u);
@@ -522,7 +661,7 @@ __global__ __launch_bounds__(kWave) void k_step(KParams p) {
                     int xx = x, yy = y;
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        t4[q] = (float)((O[ee * (W + 1) + xx] >> yy) & 1u);
+                        t4[q] = (float)((word(ee, xx) >> yy) & 1u);
                         if (++yy == H) {
                             yy = 0;
                             ++xx;
@@ -538,8 +677,50 @@ __global__ __launch_bounds__(kWave) void k_step(KParams p) {
                 const int rem = f - ee * per_env;
                 const int x = rem / H;
                 const int y = rem - x * H;
-                out[f] = (float)((O[ee * (W + 1) + x] >> y) & 1u);
+                out[f] = (float)((word(ee, x) >> y) & 1u);
             }
+        }
+    }
+    ST_STAMP(5);
+
+    // ---- state: board = obs minus the overlay (no-op where the overlay was
+    // already part of the board... see below), counters, piece ----
+    // Erasing the overlaid piece yields the post-step board for every lane:
+    // non-locking lanes and spawns (overlay cells were empty), and a death
+    // without auto-reset (R8: _set_piece(False), tetris_env.py:303).
+    __syncthreads();
+    erase(L, lane, odesc, oax, oay, hmask);
+    if (reset_now)
+        for (int x = 0; x < W; ++x) lcol(L, x, lane) = floorb;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NBQ; ++q) {
+        const int i = q * kWave + lane, x = i >> 4, c = i & 15;
+        if (x < W) {
+            uint4 v = *reinterpret_cast<const uint4 *>(&L[(x + kPad) * kWave + 4 * c]);
+            v.x &= hmask;
+            v.y &= hmask;
+            v.z &= hmask;
+            v.w &= hmask;
+            *reinterpret_cast<uint4 *>(p.board + x * sd + e0 + 4 * c) = v;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < kHotQ; ++q) {
+        const int i = q * kWave + lane, r = i >> 4, c = i & 15;
+        if (r < kHotRows) {
+            uint32_t *row = r < kStatRows ? reinterpret_cast<uint32_t *>(p.stats) + r * sd : p.piece;
+            *reinterpret_cast<uint4 *>(row + e0 + 4 * c) =
+                *reinterpret_cast<const uint4 *>(&SS[r * kWave + 4 * c]);
+        }
+    }
+    if constexpr (STAMP) {
+        ST_STAMP(6);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ST_STAMP(7);
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) p.stamps[blockIdx.x * 8 + i] = tstamp[i];
         }
     }
 }
@@ -560,7 +741,8 @@ __global__ __launch_bounds__(kWave) void k_reset(KParams p) {
     for (int i = 0; i < 7; ++i) cnt[i] = st[(ST_STAT_COUNT0 + i) * sd];
     int32_t mtidx = st[ST_STAT_MT_INDEX * sd];
     const uint32_t pw = p.piece[e];
-    const int pick = draw_shape(m, cnt, mtidx, p.mt + e0 * kMtN, S, lane);
+    const uint32_t nopre[8] = {};
+    const int pick = draw_shape(m, cnt, mtidx, p.mt + e0 * kMtN, S, lane, true, nopre, false);
     if (m) {
         st[ST_STAT_TIME * sd] = 0;
         st[ST_STAT_SCORE * sd] = 0;
@@ -735,7 +917,10 @@ hipError_t launch_reset(const KParams &p, hipStream_t s) {
 hipError_t launch_step(const KParams &p, hipStream_t s) {
     const dim3 grid((unsigned)(p.stride / kWave)), block(kWave);
     const bool f32 = p.obs_f32 != nullptr;
-    if (p.W == 10 && p.H == 20) {
+    if (p.stamps && p.W == 10 && p.H == 20) {
+        if (f32) hipLaunchKernelGGL((k_step<10, 20, true, true>), grid, block, 0, s, p);
+        else hipLaunchKernelGGL((k_step<10, 20, false, true>), grid, block, 0, s, p);
+    } else if (p.W == 10 && p.H == 20) {
         if (f32) hipLaunchKernelGGL((k_step<10, 20, true>), grid, block, 0, s, p);
         else hipLaunchKernelGGL((k_step<10, 20, false>), grid, block, 0, s, p);
     } else {

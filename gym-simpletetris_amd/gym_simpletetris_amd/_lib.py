@@ -35,7 +35,7 @@ NSTAT = 18
 MT_N = 624
 
 EXPORTS = ("st_create", "st_destroy", "st_seed", "st_reset", "st_step", "st_step_f32",
-           "st_obs_to_f32", "st_render", "st_grayscale", "st_state", "st_copy", "st_gen_actions",
+           "st_obs_to_f32", "st_render", "st_grayscale", "st_state", "st_copy", "st_gen_actions", "st_debug_stamps",
            "st_last_error", "st_abi_version")
 
 
@@ -87,6 +87,7 @@ def load(path: str = LIB_PATH):
         "st_state": ([vp, ctypes.POINTER(StateViews)], ctypes.c_int),
         "st_copy": ([vp, vp, i64, vp], ctypes.c_int),
         "st_gen_actions": ([vp, i64, i64, u64, i64, vp], ctypes.c_int),
+        "st_debug_stamps": ([vp, vp, i64], ctypes.c_int),
         "st_last_error": ([], ctypes.c_char_p),
         "st_abi_version": ([], ctypes.c_int),
     }

@@ -174,6 +174,12 @@ int st_copy(void *dst, const void *src, int64_t bytes, st_stream stream);
 int st_gen_actions(uint8_t *d_out, int64_t n, int64_t t, uint64_t seed,
                    int64_t global_offset, st_stream stream);
 
+/* Diagnostics: when the environment variable ST_STAMPS is set at st_create,
+ * st_step runs an instrumented build of the step kernel that records
+ * s_memtime at 8 phase boundaries per wave; this copies the last step's
+ * stamps ([n_waves][8] uint64) to host memory.  Timing study only. */
+int st_debug_stamps(st_ctx *ctx, uint64_t *host_out, int64_t max_words);
+
 /* Message for the last failed call on this thread ("" if none). */
 const char *st_last_error(void);
 int st_abi_version(void);

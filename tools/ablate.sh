@@ -1,0 +1,10 @@
+#!/bin/bash
+# Timing-only ablations of the step kernel (results are NOT valid games).
+set -o pipefail
+R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"; mkdir -p gpurun_out
+TAG=${TAG:-abl}
+for ab in 0 1 2 4 8 3 0; do
+  ST_ABLATE=$ab timeout -k 10 120 python bench.py --steps 500 --warmup 50 --no-extras --no-cpu-baseline ${EXTRA} \
+    | python -c "import json,sys; d=json.load(sys.stdin); print('ablate=$ab', 'us/step=%.3f' % (d['ms_per_step']*1e3), 'kernel_us=%.3f' % d['roofline']['kernel_us'])" \
+    || exit 1
+done | tee gpurun_out/ablate_$TAG.txt

@@ -1,0 +1,82 @@
+#!/usr/bin/env python
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into per-launch
+HBM bytes (profiles/<tag>_pmc.json, read by bench.py's roofline.traffic).
+
+Correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE / WRITE_SIZE are in KiB and
+derive from the L2's memory-side requests; FETCH_SIZE under-reports wide
+streaming reads by 2x on gfx950 and other widths are uncalibrated, so the
+factors are measured on tools/pmc_calib.hip's 512 MiB streams with the step
+kernel's own 4 B/lane shapes (factor = true bytes / (counter * 1024)).
+
+usage: pmc_summary.py TAG FETCH_DIR WRITE_DIR CALIB_FETCH_DIR CALIB_WRITE_DIR
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+CALIB_BYTES = 512 << 20
+
+
+def per_kernel(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    vals = defaultdict(list)
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") == counter:
+                vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return vals
+
+
+def short(name):
+    name = name.replace("st::(anonymous namespace)::", "").replace("void ", "")
+    return name.split("(")[0].strip()
+
+
+def main():
+    tag, fdir, wdir, cfdir, cwdir = sys.argv[1:6]
+    cf = per_kernel(cfdir, "FETCH_SIZE")
+    cw = per_kernel(cwdir, "WRITE_SIZE")
+
+    def factor(vals, kname, counter):
+        for k, v in vals.items():
+            if short(k) == kname:
+                m = sorted(v)[len(v) // 2]
+                return CALIB_BYTES / (m * 1024.0), m
+        raise SystemExit(f"calibration kernel {kname} missing for {counter}")
+
+    f_rd4, raw_rd4 = factor(cf, "rd4", "FETCH_SIZE")
+    f_rd16, raw_rd16 = factor(cf, "rd16", "FETCH_SIZE")
+    f_wr4, raw_wr4 = factor(cw, "wr4", "WRITE_SIZE")
+    fetch = per_kernel(fdir, "FETCH_SIZE")
+    write = per_kernel(wdir, "WRITE_SIZE")
+    out = {"tag": tag,
+           "calibration": {"fetch_factor_4B_lane": f_rd4, "fetch_factor_16B_lane": f_rd16,
+                           "write_factor_4B_lane": f_wr4, "raw_kib": {"rd4": raw_rd4, "rd16": raw_rd16,
+                                                                     "wr4": raw_wr4},
+                           "stream_bytes": CALIB_BYTES},
+           "kernels": {}}
+    for k in set(fetch) | set(write):
+        fv, wv = fetch.get(k, []), write.get(k, [])
+        if not fv or not wv:
+            continue
+        # drop the first quarter (cold caches / warm-up launches)
+        fv, wv = fv[len(fv) // 4:], wv[len(wv) // 4:]
+        fk = sum(fv) / len(fv)
+        wk = sum(wv) / len(wv)
+        rd = fk * 1024.0 * f_rd4
+        wr = wk * 1024.0 * f_wr4
+        out["kernels"][short(k)] = {
+            "launches": len(fv), "fetch_kib": fk, "write_kib": wk,
+            "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+            "hbm_bytes_per_launch": rd + wr, "full_name": k}
+    os.makedirs("profiles", exist_ok=True)
+    path = os.path.join("profiles", f"{tag}_pmc.json")
+    json.dump(out, open(path, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
