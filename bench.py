@@ -57,6 +57,16 @@ def algorithmic_bytes(width: int, height: int, p_lock: float, f32: bool) -> floa
     return always + lock * p_lock
 
 
+def rollout_bytes(width: int, height: int, p_lock: float, f32: bool, k: int) -> float:
+    """Algorithmic HBM bytes per env-step of the K-step rollout kernel: per
+    step read action 1, write packed obs 4W + reward 4 + done 1 (+ float32
+    obs 4WH); per lock MT words 8 + amortised twist 10.5; per launch the state
+    (board 4W + 14 counters + piece) read and written once, / K."""
+    step = 1 + 4 * width + 4 + 1 + (4 * width * height if f32 else 0)
+    state = 2 * (4 * width + 15 * 4)
+    return step + 18.5 * p_lock + state / k
+
+
 def cpu_baseline(seconds: float, cfg_kw: dict):
     """Oracle (C restatement of the reference step, 1 core) on a bounded sample
     of the same workload: 4,096 envs, same seeds/actions, auto-reset."""
@@ -104,6 +114,7 @@ def main():
     ap.add_argument("--obs", choices=("packed", "f32"), default="packed")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a hipGraph")
     ap.add_argument("--gather", action="store_true", help="also time a per-step RCCL gather")
+    ap.add_argument("--rollout-chunk", type=int, default=100, help="steps per st_rollout launch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="timed region only (profiling)")
@@ -161,49 +172,76 @@ def main():
             step(t, sp)
     torch.cuda.synchronize(dev)
 
-    graph = None
-    if not args.no_graph:
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=s):
-            for t in range(WU, WU + K):
-                step(t, sp)
-        torch.cuda.synchronize(dev)
-
     def spawned():
         st = eng.state_tensors(("stats",))["stats"][6:13, :n_local]
         return int(st.to(torch.int64).sum().item())
 
-    c0 = spawned()
-    # ---------------- timed region: exactly K steps ----------------
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    with torch.cuda.stream(s):
-        ev0.record(s)
-        if graph is not None:
-            graph.replay()
-        else:
-            for t in range(WU, WU + K):
-                step(t, sp)
-        ev1.record(s)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    # ---------------------------------------------------------------
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-    c1 = spawned()
-    # every lock spawns exactly one piece (new piece, or the auto-reset's)
-    p_lock = (c1 - c0) / float(n_local * K)
-    value = n_global * K / elapsed
-    ms_per_step = elapsed / K * 1e3
-    event_ms = ev0.elapsed_time(ev1) / K
+    def timed(run, nsteps):
+        """Run `run()` (enqueues exactly nsteps steps on s) inside the timed
+        region: barrier + synchronize on both sides, max over ranks."""
+        c0 = spawned()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(s):
+            ev0.record(s)
+            run()
+            ev1.record(s)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = float(tt.item())
+        # every lock spawns exactly one piece (the new piece, or the auto-reset's)
+        p_lock = (spawned() - c0) / float(n_local * nsteps)
+        return elapsed, ev0.elapsed_time(ev1), p_lock
 
+    class _Eager:  # --no-graph (PMC passes): the same launches, eagerly
+        def __init__(self, use_f32):
+            self.f = use_f32
+
+        def replay(self):
+            for t in range(WU, WU + K):
+                if self.f:
+                    C.check(L.st_step_f32(ctx, act_ptrs[t], p_obs, p_f32, p_rew, p_done, sp))
+                else:
+                    C.check(L.st_step(ctx, act_ptrs[t], p_obs, p_rew, p_done, sp))
+
+    def step_graph(use_f32):
+        if args.no_graph:
+            return _Eager(use_f32)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for t in range(WU, WU + K):
+                if use_f32:
+                    C.check(L.st_step_f32(ctx, act_ptrs[t], p_obs, p_f32, p_rew, p_done, sp))
+                else:
+                    C.check(L.st_step(ctx, act_ptrs[t], p_obs, p_rew, p_done, sp))
+        torch.cuda.synchronize(dev)
+        return g
+
+    def roofline(kern_ms, bpe, launch_steps, kname):
+        achieved = bpe * n_local * launch_steps / (kern_ms * 1e-3) / 1e9
+        traffic, pmc_file = load_pmc(kname)
+        return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
+                "kernel_us": kern_ms * 1e3, "bytes_per_env_step": bpe,
+                "bytes_per_launch": bpe * n_local * launch_steps, "traffic_source": pmc_file}
+
+    # ---------------- headline: K single steps (st_step), graph-replayed ----------------
+    graph = step_graph(f32)
+
+    def run_main():
+        graph.replay()
+    elapsed, ev_ms, p_lock = timed(run_main, K)
+    value = n_global * K / elapsed
+    event_ms = ev_ms / K
+    kname = f"k_step<10, 20, {'true' if f32 else 'false'}, false>"
     out = {
         "metric": "env-steps/sec at 65 536 parallel 10x20 boards per GPU (1->8 GPU weak scaling)",
         "value": value,
@@ -211,7 +249,7 @@ def main():
         "n_gpus": world,
         "steps": K,
         "warmup": WU,
-        "ms_per_step": ms_per_step,
+        "ms_per_step": elapsed / K * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -219,48 +257,63 @@ def main():
         "data": "synthetic (uniform splitmix64 actions, seeds 1000 + global env index)",
         "config": {
             "workload": f"{'C4' if args.config == 'c4' else 'C3'}: {n_local} parallel {W}x{H} boards "
-                        f"per GPU, ram obs ({args.obs}), auto-reset, "
+                        f"per GPU, one st_step per step, ram obs ({args.obs}), auto-reset, "
                         + ("advanced_clears+penalise_holes_increase+penalise_height_increase"
                            if args.config == "c4" else "default rewards"),
             "envs_per_gpu": n_local,
             "envs_total": n_global,
             "board": f"{W}x{H}",
             "obs": args.obs,
-            "launch": "hipGraph of K steps" if graph is not None else "eager",
+            "launch": "eager" if args.no_graph else "hipGraph of K st_step launches",
             "parallelism": f"env-shard x{world}",
         },
         "p_lock": p_lock,
         "event_ms_per_step": event_ms,
+        # graph launches run back to back (rocprofv3: ~0 gap), so the event
+        # time of the timed region / K is the kernel's average duration
+        "roofline": roofline(event_ms, algorithmic_bytes(W, H, p_lock, f32), 1, kname),
     }
+    del graph
 
-    # roofline of the step kernel.  In the hipGraph the K launches run back to
-    # back (rocprofv3 shows ~0 gap), so the HIP-event time of the timed region
-    # / K is the kernel's average launch duration.
-    kern_ms = event_ms if graph is not None else None
-    if kern_ms is None:  # eager: bracket R single launches with events
-        R = min(K, 200)
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(R)]
-        with torch.cuda.stream(s):
-            for i in range(R):
-                evs[i][0].record(s)
-                step(WU + i, sp)
-                evs[i][1].record(s)
-        torch.cuda.synchronize(dev)
-        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    bpe = algorithmic_bytes(W, H, p_lock, f32)
-    achieved = bpe * n_local / (kern_ms * 1e-3) / 1e9
-    kname = f"k_step<10, 20, {'true' if f32 else 'false'}>"
-    traffic, pmc_file = load_pmc(kname)
-    out["roofline"] = {
-        "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-        "kernel": kname, "kernel_us": kern_ms * 1e3, "bytes_per_env_step": bpe,
-        "bytes_per_launch": bpe * n_local, "traffic_source": pmc_file,
-    }
     if not args.no_extras:
+        variants = {}
+        if not f32:  # the same st_step with the reference's float32 obs fused in
+            if obs_f32 is None:  # keep the tensor alive while graphs/launches use it
+                obs_f32 = torch.zeros((n_local, W, H), dtype=torch.float32, device=dev)
+                p_f32 = ctypes.c_void_p(obs_f32.data_ptr())
+            g = step_graph(True)
+            el, ev, pl = timed(g.replay, K)
+            variants["step_f32"] = {
+                "value": n_global * K / el, "ms_per_step": el / K * 1e3, "p_lock": pl,
+                "roofline": roofline(ev / K, algorithmic_bytes(W, H, pl, True), 1,
+                                     "k_step<10, 20, true, false>")}
+            del g
+        # K-step rollout kernel (st_rollout): CH steps per launch
+        CH = min(args.rollout_chunk, K)
+        nch = K // CH
+        ro = torch.empty((CH, W, n_local), dtype=torch.int32, device=dev)
+        rr = torch.empty((CH, n_local), dtype=torch.int32, device=dev)
+        rd = torch.empty((CH, n_local), dtype=torch.uint8, device=dev)
+        for use_f32 in (False, True):
+            rf = torch.empty((CH, n_local, W, H), dtype=torch.float32, device=dev) if use_f32 else None
+            aptr = [ctypes.c_void_p(actions[WU + c * CH].data_ptr()) for c in range(nch)]
+            ptrs = [ctypes.c_void_p(x.data_ptr()) if x is not None else None for x in (ro, rf, rr, rd)]
+
+            def run_ro():
+                for c in range(nch):
+                    C.check(L.st_rollout(ctx, CH, aptr[c], *ptrs, sp))
+            with torch.cuda.stream(s):  # warm-up launch
+                C.check(L.st_rollout(ctx, CH, aptr[0], *ptrs, sp))
+            el, ev, pl = timed(run_ro, nch * CH)
+            key = "rollout_f32" if use_f32 else "rollout_packed"
+            variants[key] = {
+                "value": n_global * nch * CH / el, "ms_per_step": el / (nch * CH) * 1e3,
+                "steps_per_launch": CH, "p_lock": pl,
+                "roofline": roofline(ev / nch, rollout_bytes(W, H, pl, use_f32, CH), CH,
+                                     f"k_rollout<10, 20, {'true' if use_f32 else 'false'}>")}
+            del rf
+        out["variants"] = variants
         if args.gather and world > 1:
-            bufs_t = []
             torch.cuda.synchronize(dev)
             dist.barrier()
             g0 = time.perf_counter()
@@ -278,8 +331,7 @@ def main():
             gdt = float(tt.item())
             out["gather_variant"] = {"value": n_global * G / gdt, "ms_per_step": gdt / G * 1e3,
                                      "steps": G, "bytes_per_rank_per_step": sh.buf.numel() * 4,
-                                     "note": "eager step + RCCL gather of packed obs/reward/done to rank 0"}
-            del bufs_t
+                                     "note": "eager st_step + RCCL gather of packed obs/reward/done to rank 0"}
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cfg_kw)
     if rank == 0:

@@ -80,7 +80,6 @@ st::KParams params(const st_ctx *c) {
 
 void free_state(st_ctx *c) {
     if (c->board) (void)hipFree(c->board);
-    if (c->piece) (void)hipFree(c->piece);
     if (c->stats) (void)hipFree(c->stats);
     if (c->mt) (void)hipFree(c->mt);
     if (c->stamps) (void)hipFree(c->stamps);
@@ -108,8 +107,8 @@ int st_create(st_ctx **out, const st_config *cfg, int device, int64_t n_envs) {
     if (cfg->flags & ~0xFFu) return fail(ST_EINVAL, "unknown flag bits 0x%x", cfg->flags);
     if (cfg->autoreset != ST_AUTORESET_NONE && cfg->autoreset != ST_AUTORESET_SAME_STEP)
         return fail(ST_EINVAL, "autoreset %d unknown", cfg->autoreset);
-    if (n_envs < 1 || n_envs > (int64_t(1) << 31))
-        return fail(ST_EINVAL, "n_envs %lld outside [1, 2^31]", (long long)n_envs);
+    if (n_envs < 1 || n_envs > (int64_t(1) << 24))  // 32-bit element offsets in the kernels
+        return fail(ST_EINVAL, "n_envs %lld outside [1, 2^24] per context", (long long)n_envs);
     int ndev = 0;
     ST_HIP(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return fail(ST_EINVAL, "device %d of %d", device, ndev);
@@ -124,9 +123,11 @@ int st_create(st_ctx **out, const st_config *cfg, int device, int64_t n_envs) {
     c->stride = (n_envs + st::kWave - 1) / st::kWave * st::kWave;
     const size_t sd = (size_t)c->stride;
     hipError_t e = hipSuccess;
-    if (e == hipSuccess) e = hipMalloc(&c->board, sd * cfg->width * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMalloc(&c->piece, sd * sizeof(uint32_t));
+    // board rows padded to a multiple of 4: a wave's 16-B accesses cover 4 rows
+    const size_t wpad = (size_t)((cfg->width + 3) & ~3);
+    if (e == hipSuccess) e = hipMalloc(&c->board, sd * wpad * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&c->stats, sd * ST_NSTAT * sizeof(int32_t));
+    if (e == hipSuccess) c->piece = reinterpret_cast<uint32_t *>(c->stats) + ST_STAT_PIECE * sd;
     if (e == hipSuccess) e = hipMalloc(&c->mt, sd * st::kMtN * sizeof(uint32_t));
     if (e == hipSuccess && getenv("ST_STAMPS"))
         e = hipMalloc(&c->stamps, (sd / st::kWave) * 8 * sizeof(uint64_t));
@@ -205,6 +206,24 @@ int st_step_f32(st_ctx *c, const uint8_t *d_actions, uint32_t *d_obs, float *d_o
                 int32_t *d_reward, uint8_t *d_done, st_stream stream) {
     if (!d_obs_f32) return fail(ST_EINVAL, "st_step_f32: null d_obs_f32");
     return step_impl(c, d_actions, d_obs, d_obs_f32, d_reward, d_done, stream);
+}
+
+int st_rollout(st_ctx *c, int32_t k, const uint8_t *d_actions, uint32_t *d_obs, float *d_obs_f32,
+               int32_t *d_reward, uint8_t *d_done, st_stream stream) {
+    if (!c || !d_actions) return fail(ST_EINVAL, "st_rollout: null argument");
+    if (k < 1) return fail(ST_EINVAL, "st_rollout: k = %d < 1", k);
+    if (!c->seeded || !c->reset_once)
+        return fail(ST_ESTATE, "st_rollout before st_seed + st_reset (tetris_env.py:244 needs an anchor)");
+    DeviceGuard g(c->device);
+    st::KParams p = params(c);
+    p.k = k;
+    p.actions = d_actions;
+    p.obs = d_obs;
+    p.obs_f32 = d_obs_f32;
+    p.reward = d_reward;
+    p.done = d_done;
+    ST_HIP(st::launch_rollout(p, (hipStream_t)stream));
+    return ST_OK;
 }
 
 int st_obs_to_f32(st_ctx *c, const uint32_t *d_obs, float *d_out, st_stream stream) {

@@ -12,9 +12,8 @@ constexpr int kPad = 4;        // wall columns on each side of the LDS board
 constexpr int kMaxW = 32;
 constexpr int kMaxH = 28;
 constexpr int kMtN = 624;
-constexpr int kStatRows = 14;                // stats rows 0..13 move with every step
-constexpr int kPieceRow = kStatRows;         // staged row 14 = piece word
-constexpr int kHotRows = kStatRows + 1;
+constexpr int kPieceRow = ST_STAT_PIECE;     // rows 0..14 (counters + piece) move every step
+constexpr int kHotRows = ST_STAT_PIECE + 1;
 constexpr int kHotQ = (kHotRows * 16 + kWave - 1) / kWave;  // 16-B slots per lane
 
 struct KParams {
@@ -27,6 +26,7 @@ struct KParams {
                         // 4 = no twist, 8 = no obs output
     uint64_t *stamps;   // DIAGNOSTIC build only (env ST_STAMPS at st_create): per-wave
                         // s_memtime at 8 phase boundaries of the step kernel
+    int32_t k;          // st_rollout: number of steps
     int64_t n;          // real envs
     int64_t stride;     // padded env count (multiple of 64) = SoA row stride
     // state
@@ -47,6 +47,7 @@ struct KParams {
 hipError_t launch_seed(const KParams &p, hipStream_t s);
 hipError_t launch_reset(const KParams &p, hipStream_t s);
 hipError_t launch_step(const KParams &p, hipStream_t s);
+hipError_t launch_rollout(const KParams &p, hipStream_t s);
 hipError_t launch_obs_f32(const KParams &p, const uint32_t *obs, float *out, hipStream_t s);
 hipError_t launch_render(const KParams &p, hipStream_t s);
 hipError_t launch_grayscale(const KParams &p, const uint32_t *obs, int size, int channels,

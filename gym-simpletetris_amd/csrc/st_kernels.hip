@@ -18,6 +18,12 @@
 // bounds checks and hard_drop is a count-trailing-zeros per piece column.
 #include "st_internal.h"
 
+// st_rollout draws from a per-lane LDS ring of MT words (1) or, like st_step,
+// from words prefetched when the lane locks (0).  Diagnostic A/B switch.
+#ifndef ST_RING
+#define ST_RING 1
+#endif
+
 namespace st {
 namespace {
 
@@ -30,13 +36,14 @@ constexpr int kShapes[7][4][2] = {
     {{0, 0}, {0, -1}, {-1, 0}, {-1, -1}},
 };
 
-// One descriptor per (piece, rot): four 8-bit column records
-//   bits 0-2 dx+3, bits 3-5 (top dy)+3, bits 6-7 run length-1.
+// One descriptor per (piece, rot) = {m, g}, four column records each:
+//   m: byte j = the column's cells as a bit mask biased by 3 (bit dy+3);
+//   g: 6 bits per column j: dx+3 (bits 6j..6j+2), bottom dy+3 (6j+3..6j+5).
 // Tetromino columns are vertically contiguous runs (checked below); pieces
 // with fewer than 4 columns repeat their last column (OR/AND/min idempotent).
 // rot r = r applications of rotated(cclk=False) (tetris_env.py:22-26).
 struct PieceTab {
-    uint32_t d[28];
+    uint32_t m[28], g[28];
     bool ok;
 };
 
@@ -50,24 +57,32 @@ constexpr PieceTab make_piece_tab() {
             cy[c] = kShapes[p][c][1];
         }
         for (int r = 0; r < 4; ++r) {
-            uint32_t desc = 0, last = 0;
+            uint32_t m = 0, g = 0, lm = 0, lg = 0;
             int ncol = 0;
             for (int dx = -3; dx <= 3; ++dx) {
                 int ymin = 99, ymax = -99, cnt = 0;
+                uint32_t bits = 0;
                 for (int c = 0; c < 4; ++c)
                     if (cx[c] == dx) {
                         ++cnt;
                         ymin = cy[c] < ymin ? cy[c] : ymin;
                         ymax = cy[c] > ymax ? cy[c] : ymax;
+                        bits |= 1u << (cy[c] + 3);
                     }
                 if (!cnt) continue;
                 if (cnt != ymax - ymin + 1 || ymin < -3 || ymax > 3) t.ok = false;
-                last = (uint32_t)(dx + 3) | ((uint32_t)(ymin + 3) << 3) | ((uint32_t)(ymax - ymin) << 6);
-                desc |= last << (8 * ncol);
+                lm = bits;
+                lg = (uint32_t)(dx + 3) | ((uint32_t)(ymax + 3) << 3);
+                m |= lm << (8 * ncol);
+                g |= lg << (6 * ncol);
                 ++ncol;
             }
-            for (int j = ncol; j < 4; ++j) desc |= last << (8 * j);
-            t.d[p * 4 + r] = desc;
+            for (int j = ncol; j < 4; ++j) {
+                m |= lm << (8 * j);
+                g |= lg << (6 * j);
+            }
+            t.m[p * 4 + r] = m;
+            t.g[p * 4 + r] = g;
             for (int c = 0; c < 4; ++c) {  // rotated(cclk=False): (i, j) -> (j, -i)
                 const int i = cx[c], j = cy[c];
                 cx[c] = j;
@@ -79,31 +94,19 @@ constexpr PieceTab make_piece_tab() {
 }
 constexpr PieceTab kTab = make_piece_tab();
 static_assert(kTab.ok, "every tetromino column must be a contiguous run within [-3, 3]");
-__constant__ uint32_t c_tab[28] = {
-    kTab.d[0],  kTab.d[1],  kTab.d[2],  kTab.d[3],  kTab.d[4],  kTab.d[5],  kTab.d[6],
-    kTab.d[7],  kTab.d[8],  kTab.d[9],  kTab.d[10], kTab.d[11], kTab.d[12], kTab.d[13],
-    kTab.d[14], kTab.d[15], kTab.d[16], kTab.d[17], kTab.d[18], kTab.d[19], kTab.d[20],
-    kTab.d[21], kTab.d[22], kTab.d[23], kTab.d[24], kTab.d[25], kTab.d[26], kTab.d[27]};
+#define ST_TAB28(a) {a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8], a[9], a[10], a[11], \
+                     a[12], a[13], a[14], a[15], a[16], a[17], a[18], a[19], a[20], a[21], a[22], \
+                     a[23], a[24], a[25], a[26], a[27]}
+__constant__ uint32_t c_tab_m[28] = ST_TAB28(kTab.m);
+__constant__ uint32_t c_tab_g[28] = ST_TAB28(kTab.g);
 
-// Piece table entry `lane` (lanes 0..27) materialised from immediates: no
-// memory round trip at kernel entry.
-__device__ __forceinline__ uint32_t tab_entry(int lane) {
-    uint32_t v = 0;
-#pragma unroll
-    for (int j = 0; j < 28; ++j) v = lane == j ? kTab.d[j] : v;
-    return v;
-}
-
-__device__ __forceinline__ int col_dx(uint32_t c) { return (int)(c & 7u) - 3; }
-__device__ __forceinline__ int col_top(uint32_t c) { return (int)((c >> 3) & 7u) - 3; }
-__device__ __forceinline__ int col_bot(uint32_t c) { return col_top(c) + (int)(c >> 6); }
-
-// Bits of one piece column's cells at anchor row y; cells with y < 0 vanish
-// (is_occupied skips them, tetris_env.py:32-33; _set_piece clips them, :326).
-__device__ __forceinline__ uint32_t run_bits(uint32_t c, int y) {
-    const int top = y + col_top(c);
-    const uint32_t m = (2u << (c >> 6)) - 1u;
-    return top >= 0 ? (m << top) : (m >> (-top));
+// Column j of a descriptor: dx, bottom dy, and its cells at anchor row y as
+// board-row bits; cells with y < 0 vanish (is_occupied skips them,
+// tetris_env.py:32-33; _set_piece clips them, :326).
+__device__ __forceinline__ int pc_dx(uint32_t g, int j) { return (int)((g >> (6 * j)) & 7u) - 3; }
+__device__ __forceinline__ int pc_bot(uint32_t g, int j) { return (int)((g >> (6 * j + 3)) & 7u) - 3; }
+__device__ __forceinline__ uint32_t pc_bits(uint32_t m, int j, int y) {
+    return (uint32_t)((uint64_t)((m >> (8 * j)) & 0xFFu) << y >> 3);
 }
 
 __device__ __forceinline__ uint32_t &lcol(uint32_t *L, int x, int lane) {
@@ -114,32 +117,29 @@ __device__ __forceinline__ uint32_t &lcol(uint32_t *L, int x, int lane) {
 // one batch of LDS reads), and the collision / drop tests on them:
 //  collides_v = is_occupied (tetris_env.py:29-36) with the floor bits and the
 //    all-ones wall columns standing in for the bounds checks; cells with y < 0
-//    vanish in run_bits (R2);
+//    vanish in pc_bits (R2);
 //  drop_v = the number of free soft_drops below a legal position, i.e.
 //    hard_drop's loop count (tetris_env.py:54-59): only each column's lowest
 //    cell can meet an obstacle first, and the first obstacle row is the lowest
 //    set bit of (column | floor) at or below it.  A column outside the board
 //    (legal only while its cells are above row 0) reads a wall and stops the
 //    piece as its lowest cell would enter row 0.
-__device__ __forceinline__ void read_cols(const uint32_t *L, int lane, uint32_t d, int x,
+__device__ __forceinline__ void read_cols(const uint32_t *L, int lane, uint32_t g, int x,
                                           uint32_t (&v)[4]) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t c = (d >> (8 * j)) & 0xFFu;
-        v[j] = L[(x + col_dx(c) + kPad) * kWave + lane];
-    }
+    for (int j = 0; j < 4; ++j) v[j] = L[(x + pc_dx(g, j) + kPad) * kWave + lane];
 }
-__device__ __forceinline__ bool collides_v(uint32_t d, int y, const uint32_t (&v)[4]) {
+__device__ __forceinline__ bool collides_v(uint32_t m, int y, const uint32_t (&v)[4]) {
     uint32_t hit = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) hit |= run_bits((d >> (8 * j)) & 0xFFu, y) & v[j];
+    for (int j = 0; j < 4; ++j) hit |= pc_bits(m, j, y) & v[j];
     return hit != 0;
 }
-__device__ __forceinline__ int drop_v(uint32_t d, int y, const uint32_t (&v)[4]) {
+__device__ __forceinline__ int drop_v(uint32_t g, int y, const uint32_t (&v)[4]) {
     int dist = 1 << 20;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int yb = y + col_bot((d >> (8 * j)) & 0xFFu);
+        const int yb = y + pc_bot(g, j);
         const int s = yb + 1 > 0 ? yb + 1 : 0;
         const int k = __builtin_ctz(v[j] & (~0u << s)) - yb - 1;
         dist = k < dist ? k : dist;
@@ -147,22 +147,21 @@ __device__ __forceinline__ int drop_v(uint32_t d, int y, const uint32_t (&v)[4])
     return dist;
 }
 
-// _set_piece(True) (tetris_env.py:323-327): cells inside the board only.
-__device__ __forceinline__ void paint(uint32_t *L, int lane, uint32_t d, int x, int y, uint32_t hmask) {
+// _set_piece(True) (tetris_env.py:323-327): cells inside the board only,
+// as no-return LDS atomics.
+__device__ __forceinline__ void paint(uint32_t *L, int lane, uint32_t m, uint32_t g, int x, int y,
+                                      uint32_t hmask) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t c = (d >> (8 * j)) & 0xFFu;
-        atomicOr(&lcol(L, x + col_dx(c), lane), run_bits(c, y) & hmask);  // ds_or_b32
-    }
+    for (int j = 0; j < 4; ++j)
+        atomicOr(&L[(x + pc_dx(g, j) + kPad) * kWave + lane], pc_bits(m, j, y) & hmask);  // ds_or_b32
 }
 
-// _set_piece(False): erase the cells (only matters on a death step, R8).
-__device__ __forceinline__ void erase(uint32_t *L, int lane, uint32_t d, int x, int y, uint32_t hmask) {
+// _set_piece(False): erase the cells.
+__device__ __forceinline__ void erase(uint32_t *L, int lane, uint32_t m, uint32_t g, int x, int y,
+                                      uint32_t hmask) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t c = (d >> (8 * j)) & 0xFFu;
-        atomicAnd(&lcol(L, x + col_dx(c), lane), ~(run_bits(c, y) & hmask));  // ds_and_b32
-    }
+    for (int j = 0; j < 4; ++j)
+        atomicAnd(&L[(x + pc_dx(g, j) + kPad) * kWave + lane], ~(pc_bits(m, j, y) & hmask));
 }
 
 // _clear_lines row compaction (tetris_env.py:205-216) on one column word:
@@ -179,8 +178,9 @@ __device__ __forceinline__ uint32_t compact(uint32_t v, uint32_t full) {
 
 // _count_holes (tetris_env.py:218-220) for one column: empty cells below the
 // topmost filled cell.
-__device__ __forceinline__ int col_holes(uint32_t v, int H) {
-    return v ? H - __builtin_ctz(v) - __builtin_popcount(v) : 0;
+__device__ __forceinline__ int col_holes(uint32_t v, uint32_t hmask) {
+    const uint32_t above = (v & (0u - v)) - 1u;  // rows above the topmost cell (all if v == 0)
+    return __builtin_popcount(hmask & ~(v | above));
 }
 
 // ---------------------------------------------------------------- MT19937
@@ -301,6 +301,7 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], int32_t 
         }
         have_pre = false;
         if (tw) {
+            bool mine = false;  // this lane's state was twisted in this round
             do {
                 const int l = __builtin_ctzll(tw);
                 tw &= tw - 1;
@@ -308,11 +309,12 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], int32_t 
                 if (lane == l) {  // the twisted lane takes its first words from LDS
 #pragma unroll
                     for (int j = 0; j < 8; ++j) w[j] = S[j];
-                    have = true;
+                    mine = true;
                 }
                 __syncthreads();  // S is reused by the next lane's twist
             } while (tw);
-            if (have) {
+            if (mine) {
+                have = true;
                 mtidx = 0;
                 fresh = true;
             }
@@ -326,16 +328,170 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], int32_t 
             for (int j = 0; j < 8; ++j)
                 w[j] = (mtidx + j < kMtN) ? __builtin_nontemporal_load(g + mtidx + j) : 0u;
         }
-        if (pending) {
+        // consume words until every lane has its piece (most waves stop after
+        // 3-5 of the 8: each getrandbits(k) is accepted with p >= 1/2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (!__ballot(pending && mtidx < kMtN)) break;
+            if (pending && mtidx < kMtN) {
+                const uint32_t y = mt_temper(w[j]) >> (32 - k);
+                ++mtidx;
+                if (y < n) {
+                    pending = false;
+                    r = y;
+                }
+            }
+        }
+    }
+    if (!need) return 0;
+    int32_t rr = (int32_t)r + 1;
+    int pick = 6;
+    bool found = false;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        rr -= 5 + maxc - cnt[i];
+        if (!found && rr <= 0) {
+            pick = i;
+            found = true;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 7; ++i) cnt[i] += (i == pick);
+    return pick;
+}
+
+// ---------------------------------------------------------------- MT word ring
+// st_rollout keeps each lane's upcoming MT words in LDS: ring slot s of lane l
+// is R[s * 64 + l] and holds word index i at s = i & 31 for i in [mtidx, hi).
+// Refills fetch the aligned 16-word chunk at `hi` (64 B, one cache line) with
+// one nt dwordx4 load per 4 words, a step before the words can be needed, and
+// are committed into the ring at the next draw -- so draws need no dependent
+// load and each line of MT state is fetched once.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct MtRing {
+    int32_t hi;       // ring holds the words with index < hi (>= mtidx unconsumed)
+    int32_t pend_lo;  // start index of the refill in flight, -1 if none
+    u32x4 pend[4];
+};
+
+__device__ __forceinline__ void ring_put(uint32_t *R, int lane, int idx, uint32_t w) {
+    R[(idx & 31) * kWave + lane] = w;
+}
+
+__device__ __forceinline__ void ring_init(MtRing &r, uint32_t *R, const uint32_t *g, int32_t mtidx,
+                                          int lane) {
+    const int lo = mtidx & ~15;  // 624 = 39 * 16: chunks never straddle the end
+    const int nfill = kMtN - lo < 32 ? kMtN - lo : 32;  // 0, 16 or 32 words
+    uint4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        v[j] = 4 * j < nfill ? *reinterpret_cast<const uint4 *>(g + lo + 4 * j) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (4 * j < nfill) {
+            ring_put(R, lane, lo + 4 * j, v[j].x);
+            ring_put(R, lane, lo + 4 * j + 1, v[j].y);
+            ring_put(R, lane, lo + 4 * j + 2, v[j].z);
+            ring_put(R, lane, lo + 4 * j + 3, v[j].w);
+        }
+    }
+    r.hi = lo + nfill;
+    r.pend_lo = -1;
+}
+
+// After a draw: start fetching the next chunk once <= 16 words remain.
+__device__ __forceinline__ void ring_refill(MtRing &r, const uint32_t *g, int32_t mtidx) {
+    if (mtidx > r.hi) r.hi = mtidx & ~15;  // a draw ran past the ring (fallback loads)
+    if (r.pend_lo < 0 && r.hi < kMtN && r.hi - mtidx <= 16) {
+        r.pend_lo = r.hi;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            r.pend[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(g + r.hi + 4 * j));
+    }
+}
+
+__device__ __forceinline__ void ring_commit(MtRing &r, uint32_t *R, int lane) {
+    if (r.pend_lo >= 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            ring_put(R, lane, r.pend_lo + 4 * j, r.pend[j].x);
+            ring_put(R, lane, r.pend_lo + 4 * j + 1, r.pend[j].y);
+            ring_put(R, lane, r.pend_lo + 4 * j + 2, r.pend[j].z);
+            ring_put(R, lane, r.pend_lo + 4 * j + 3, r.pend[j].w);
+        }
+        r.hi = r.pend_lo + 16;
+        r.pend_lo = -1;
+    }
+}
+
+// draw_shape with the words taken from the ring (see draw_shape for the
+// algorithm).  Words past the ring (a single draw consuming > 16 words) are
+// loaded directly; exhausted states are twisted cooperatively and the
+// twisted lane refills its ring from the new state in LDS.
+__device__ __forceinline__ int draw_shape_ring(bool need, int32_t (&cnt)[7], int32_t &mtidx,
+                                               uint32_t *mt_wave, uint32_t *S, uint32_t *R,
+                                               MtRing &ring, int lane, bool twist) {
+    ring_commit(ring, R, lane);
+    int32_t maxc = cnt[0], sumc = cnt[0];
+#pragma unroll
+    for (int i = 1; i < 7; ++i) {
+        maxc = cnt[i] > maxc ? cnt[i] : maxc;
+        sumc += cnt[i];
+    }
+    const uint32_t n = (uint32_t)(35 + 7 * maxc - sumc);
+    const int k = 32 - __builtin_clz(n);
+    const uint32_t *g = mt_wave + (size_t)lane * kMtN;
+    bool pending = need;
+    uint32_t r = 0;
+    while (__ballot(pending)) {
+        if (!twist && pending && mtidx >= kMtN) mtidx = 0;  // ablation: skip the twist
+        uint64_t tw = __ballot(pending && mtidx >= kMtN);
+        if (tw) {
+            bool mine = false;
+            do {
+                const int l = __builtin_ctzll(tw);
+                tw &= tw - 1;
+                coop_twist(mt_wave + (size_t)l * kMtN, S, lane);
+                if (lane == l) {
+#pragma unroll 4
+                    for (int i = 0; i < 32; ++i) ring_put(R, lane, i, S[i]);
+                    mine = true;
+                }
+                __syncthreads();  // S is reused by the next lane's twist
+            } while (tw);
+            // the twist's stores must reach L2 before any nt reload of them
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (mine) {
+                mtidx = 0;
+                ring.hi = 32;
+                ring.pend_lo = -1;
+            }
+        }
+        uint32_t w[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int idx = mtidx + j;
+            w[j] = idx < ring.hi ? R[(idx & 31) * kWave + lane] : 0u;
+        }
+        if (__ballot(pending && mtidx + 8 > ring.hi && ring.hi < kMtN)) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                if (pending && mtidx < kMtN) {
-                    const uint32_t y = mt_temper(w[j]) >> (32 - k);
-                    ++mtidx;
-                    if (y < n) {
-                        pending = false;
-                        r = y;
-                    }
+                const int idx = mtidx + j;
+                if (pending && idx >= ring.hi && idx < kMtN) w[j] = __builtin_nontemporal_load(g + idx);
+            }
+        }
+        // consume words until every lane has its piece (most waves stop after
+        // 3-5 of the 8: each getrandbits(k) is accepted with p >= 1/2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (!__ballot(pending && mtidx < kMtN)) break;
+            if (pending && mtidx < kMtN) {
+                const uint32_t y = mt_temper(w[j]) >> (32 - k);
+                ++mtidx;
+                if (y < n) {
+                    pending = false;
+                    r = y;
                 }
             }
         }
@@ -373,8 +529,12 @@ __device__ __forceinline__ uint32_t pack_piece(int id, int rot, int ax, int ay, 
         }                                                              \
     } while (0)
 
-template <int WT, int HT, bool F32, bool STAMP = false>
-__global__ __launch_bounds__(kWave) void k_step(KParams p) {
+// One wave = 64 envs.  KSTEPS == 1: TetrisEngine.step once (st_step);
+// KSTEPS == 0: p.k consecutive steps (st_rollout) with the board and counters
+// kept in LDS between steps, actions read one step ahead, and per-step
+// outputs at [t].  State is loaded once at the start and stored once at the end.
+template <int WT, int HT, bool F32, bool STAMP, int KSTEPS>
+__device__ __forceinline__ void run_steps(const KParams &p) {
     [[maybe_unused]] uint64_t tstamp[8] = {};
     ST_STAMP(0);
     // LDS: board columns L[x + kPad][lane] (walls at both ends), the staged
@@ -383,7 +543,12 @@ __global__ __launch_bounds__(kWave) void k_step(KParams p) {
     __shared__ __attribute__((aligned(16))) uint32_t L[(kMaxW + 2 * kPad) * kWave];
     __shared__ __attribute__((aligned(16))) uint32_t SS[kHotQ * 4 * kWave];
     __shared__ uint32_t S[kMtN];
-    __shared__ uint32_t T[28];
+    __shared__ uint2 T2[28];
+    // float32 obs writer (F32): per-lane obs words at stride W+1 (conflict-
+    // free transposed reads) and the 16 float4 patterns of a 4-bit nibble.
+    __shared__ uint32_t O[F32 ? kWave * (kMaxW + 1) : 1];
+    __shared__ __attribute__((aligned(16))) float4 F4[F32 ? 16 : 1];
+    __shared__ uint32_t R[(KSTEPS != 1 && F32 && ST_RING) ? 32 * kWave : 1];  // MT word ring
     const int W = WT ? WT : p.W;
     const int H = HT ? HT : p.H;
     const int lane = threadIdx.x;
@@ -395,37 +560,37 @@ __global__ __launch_bounds__(kWave) void k_step(KParams p) {
     const uint32_t floorb = ~hmask;
 
     // ---- loads: 16 B per lane (a wave's slice of one SoA row is 256 B) ----
-    // Unconditional (clamped) so the compiler issues them all back to back:
-    // board slots past the last column land in the right-wall columns, which
-    // are written after them; counter slots past row 14 land in padding row 15.
-    constexpr int NBQ = ((WT ? WT : kMaxW) * 16 + kWave - 1) / kWave;  // board x4 slots
+    // Lane l covers row 4q + l/16, envs 4(l%16)..+3: one per-lane 32-bit offset
+    // `loff` serves every 4-row group q (the group's base is wave-uniform), so
+    // addresses are SGPR base + VGPR offset.  The board allocation is padded
+    // to a multiple of 4 rows; rows >= W land in the right-wall LDS columns,
+    // which are written after them.  Counter rows: 0..14 plus row 15 (unused).
+    const uint32_t loff = (uint32_t)(lane >> 4) * (uint32_t)sd + 4u * (uint32_t)(lane & 15);
+    constexpr int NBQ = ((WT ? WT : kMaxW) + 3) / 4;  // board 4-row groups
+    const uint32_t *bsrc = p.board + e0;
+    const uint32_t *ssrc = reinterpret_cast<const uint32_t *>(p.stats) + e0;
     uint4 bv[NBQ];
 #pragma unroll
-    for (int q = 0; q < NBQ; ++q) {
-        const int i = q * kWave + lane, c = i & 15;
-        const int x = (i >> 4) < W ? (i >> 4) : W - 1;
-        bv[q] = *reinterpret_cast<const uint4 *>(p.board + x * sd + e0 + 4 * c);
-    }
+    for (int q = 0; q < NBQ; ++q)
+        if (WT || 4 * q < W) bv[q] = *reinterpret_cast<const uint4 *>(bsrc + (size_t)(4 * q) * sd + loff);
     uint4 sv[kHotQ];
 #pragma unroll
-    for (int q = 0; q < kHotQ; ++q) {
-        const int i = q * kWave + lane, c = i & 15;
-        const int r = (i >> 4) < kHotRows ? (i >> 4) : kHotRows - 1;
-        const uint32_t *row = r < kStatRows ? reinterpret_cast<const uint32_t *>(p.stats) + r * sd
-                                            : p.piece;
-        sv[q] = *reinterpret_cast<const uint4 *>(row + e0 + 4 * c);
-    }
-    const uint32_t act = real ? (uint32_t)p.actions[e] : 6u;
-    if (lane < 28) T[lane] = tab_entry(lane);
+    for (int q = 0; q < kHotQ; ++q)
+        sv[q] = *reinterpret_cast<const uint4 *>(ssrc + (size_t)(4 * q) * sd + loff);
+    const int K = KSTEPS ? KSTEPS : p.k;
+    uint32_t act_next = real ? (uint32_t)p.actions[e] : 6u;
+    const uint2 tabv = make_uint2(c_tab_m[lane < 28 ? lane : 0], c_tab_g[lane < 28 ? lane : 0]);
+    const int lrow = lane >> 4, lcc = 4 * (lane & 15);  // this lane's row-in-group, env slot
 #pragma unroll
     for (int q = 0; q < NBQ; ++q) {
-        const int i = q * kWave + lane, x = i >> 4, c = i & 15;
-        uint4 v = bv[q];
-        v.x |= floorb;
-        v.y |= floorb;
-        v.z |= floorb;
-        v.w |= floorb;
-        *reinterpret_cast<uint4 *>(&L[(x + kPad) * kWave + 4 * c]) = v;
+        if (WT || 4 * q < W) {
+            uint4 v = bv[q];
+            v.x |= floorb;
+            v.y |= floorb;
+            v.z |= floorb;
+            v.w |= floorb;
+            *reinterpret_cast<uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]) = v;
+        }
     }
 #pragma unroll
     for (int x = 0; x < kPad; ++x) {  // walls (after the board slots, see above)
@@ -433,13 +598,25 @@ __global__ __launch_bounds__(kWave) void k_step(KParams p) {
         L[(W + kPad + x) * kWave + lane] = ~0u;
     }
 #pragma unroll
-    for (int q = 0; q < kHotQ; ++q) {
-        const int i = q * kWave + lane, c = i & 15;
-        *reinterpret_cast<uint4 *>(&SS[(i >> 4) * kWave + 4 * c]) = sv[q];
+    for (int q = 0; q < kHotQ; ++q)
+        *reinterpret_cast<uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]) = sv[q];
+    if (lane < 28) T2[lane] = tabv;
+    if constexpr (F32) {
+        if (lane < 16)
+            F4[lane] = make_float4((float)(lane & 1), (float)((lane >> 1) & 1),
+                                   (float)((lane >> 2) & 1), (float)((lane >> 3) & 1));
     }
     __syncthreads();
     auto ss = [&](int r) -> uint32_t & { return SS[r * kWave + lane]; };
+    [[maybe_unused]] MtRing ring;
+    // ring only where it pays (A/B): the HBM-bound f32 rollout
+    constexpr bool kRing = KSTEPS != 1 && F32 && ST_RING;
+    if constexpr (kRing) ring_init(ring, R, p.mt + e * kMtN, (int32_t)ss(ST_STAT_MT_INDEX), lane);
 
+    for (int t = 0; t < K; ++t) {
+    const uint32_t act = act_next;
+    if (KSTEPS != 1 && t + 1 < K) act_next = real ? (uint32_t)p.actions[(int64_t)(t + 1) * p.n + e] : 6u;
+    uint32_t *const obs_t = p.obs ? p.obs + (int64_t)t * W * p.n : nullptr;
     const uint32_t pw = ss(kPieceRow);
     int32_t time = (int32_t)ss(ST_STAT_TIME);
     const int id = (int)(pw & 7u);
@@ -456,19 +633,19 @@ __global__ __launch_bounds__(kWave) void k_step(KParams p) {
     const bool tries = act == 0u || act == 1u || act == 4u || act == 5u;
     const int cx = ax + (act == 0u ? -1 : (act == 1u ? 1 : 0));
     const int cr = act == 4u ? ((rot + 1) & 3) : (act == 5u ? ((rot + 3) & 3) : rot);
-    uint32_t desc = T[id * 4 + rot];
-    const uint32_t cdesc = T[id * 4 + cr];
+    uint2 desc = T2[id * 4 + rot];
+    const uint2 cdesc = T2[id * 4 + cr];
     uint32_t cur[4], cand[4];
-    read_cols(L, lane, desc, ax, cur);
-    read_cols(L, lane, cdesc, cx, cand);
+    read_cols(L, lane, desc.y, ax, cur);
+    read_cols(L, lane, cdesc.y, cx, cand);
     int d;
-    if (tries && !collides_v(cdesc, ay, cand)) {
+    if (tries && !collides_v(cdesc.x, ay, cand)) {
         ax = cx;
         rot = cr;
         desc = cdesc;
-        d = drop_v(cdesc, ay, cand);
+        d = drop_v(cdesc.y, ay, cand);
     } else {
-        d = drop_v(desc, ay, cur);
+        d = drop_v(desc.y, ay, cur);
     }
     if (act == 2u) {                 // hard_drop :54-59
         ay += d;
@@ -495,8 +672,8 @@ __global__ __launch_bounds__(kWave) void k_step(KParams p) {
     // lock path (every locking lane draws: a spawn, or the same-step reset's).
     int32_t mtidx = (int32_t)ss(ST_STAT_MT_INDEX);
     uint32_t pre[8];
-    const bool want_pre = locknow && mtidx < kMtN && !(p.ablate & 2u);
-    prefetch_words(p.mt + e * kMtN, mtidx, want_pre, pre);
+    const bool want_pre = !kRing && locknow && mtidx < kMtN && !(p.ablate & 2u);
+    if constexpr (!kRing) prefetch_words(p.mt + e * kMtN, mtidx, want_pre, pre);
 
     // ---- lock path (tetris_env.py:263-299) ----
     bool died = false, spawn = false;
@@ -507,7 +684,7 @@ __global__ __launch_bounds__(kWave) void k_step(KParams p) {
         holes = (int32_t)ss(ST_STAT_HOLES);
         height = (int32_t)ss(ST_STAT_PIECE_HEIGHT);
         deaths = (int32_t)ss(ST_STAT_DEATHS);
-        paint(L, lane, desc, ax, ay, hmask);
+        paint(L, lane, desc.x, desc.y, ax, ay, hmask);
         uint32_t andv = hmask, orv = 0;
         int32_t nh = 0;
 #pragma unroll 8
@@ -515,7 +692,7 @@ __global__ __launch_bounds__(kWave) void k_step(KParams p) {
             const uint32_t v = lcol(L, x, lane) & hmask;
             andv &= v;
             orv |= v;
-            nh += col_holes(v, H);
+            nh += col_holes(v, hmask);
         }
         int32_t ncl = 0;
         if (andv) {  // full rows: compact, recount
@@ -527,7 +704,7 @@ __global__ __launch_bounds__(kWave) void k_step(KParams p) {
                 const uint32_t v = compact(lcol(L, x, lane) & hmask, andv);
                 lcol(L, x, lane) = v | floorb;
                 orv |= v;
-                nh += col_holes(v, H);
+                nh += col_holes(v, hmask);
             }
             lines += ncl;
         }
@@ -570,16 +747,24 @@ __global__ __launch_bounds__(kWave) void k_step(KParams p) {
     int32_t cnt[7];
 #pragma unroll
     for (int i = 0; i < 7; ++i) cnt[i] = draw ? (int32_t)ss(ST_STAT_COUNT0 + i) : 0;
-    const int pick = (p.ablate & 2u) ? 0
-                                      : draw_shape(draw, cnt, mtidx, p.mt + e0 * kMtN, S, lane,
-                                                   !(p.ablate & 4u), pre, want_pre);
+    int pick = 0;
+    if (!(p.ablate & 2u)) {
+        if constexpr (!kRing) {
+            pick = draw_shape(draw, cnt, mtidx, p.mt + e0 * kMtN, S, lane, !(p.ablate & 4u), pre,
+                              want_pre);
+        } else {
+            pick = draw_shape_ring(draw, cnt, mtidx, p.mt + e0 * kMtN, S, R, ring, lane,
+                                   !(p.ablate & 4u));
+            ring_refill(ring, p.mt + e * kMtN, mtidx);
+        }
+    }
     ST_STAMP(4);
-    uint32_t odesc = desc;
+    uint2 odesc = desc;
     int oax = ax, oay = ay;
     uint32_t pw_out = pack_piece(id, rot, ax, ay, lock);
     if (draw) pw_out = pack_piece(pick, 0, W / 2, 0, lock);
     if (spawn) {
-        odesc = T[pick * 4];
+        odesc = T2[pick * 4];
         oax = W / 2;
         oay = 0;
     }
@@ -606,72 +791,59 @@ __global__ __launch_bounds__(kWave) void k_step(KParams p) {
     }
 
     // ---- observation (tetris_env.py:301-302): board + current piece ----
-    paint(L, lane, odesc, oax, oay, hmask);
+    paint(L, lane, odesc.x, odesc.y, oax, oay, hmask);
     __syncthreads();
     const bool wide_obs = (p.n & 3) == 0 && e0 + kWave <= p.n &&
                           (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0;
-    if (p.obs && !(p.ablate & 8u)) {
+    if (obs_t && !(p.ablate & 8u)) {
         if (wide_obs) {
+            const uint32_t noff = (uint32_t)lrow * (uint32_t)p.n + (uint32_t)lcc;
+            uint32_t *odst = obs_t + e0;
 #pragma unroll
             for (int q = 0; q < NBQ; ++q) {
-                const int i = q * kWave + lane, x = i >> 4, c = i & 15;
-                if (x < W) {
-                    uint4 v = *reinterpret_cast<const uint4 *>(&L[(x + kPad) * kWave + 4 * c]);
+                if ((WT || 4 * q < W) && 4 * q + lrow < W) {
+                    uint4 v = *reinterpret_cast<const uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]);
                     v.x &= hmask;
                     v.y &= hmask;
                     v.z &= hmask;
                     v.w &= hmask;
-                    *reinterpret_cast<uint4 *>(p.obs + x * p.n + e0 + 4 * c) = v;
+                    *reinterpret_cast<uint4 *>(odst + (size_t)(4 * q) * p.n + noff) = v;
                 }
             }
         } else if (real) {
-            for (int x = 0; x < W; ++x) p.obs[x * p.n + e] = lcol(L, x, lane) & hmask;
+            for (int x = 0; x < W; ++x) obs_t[x * p.n + e] = lcol(L, x, lane) & hmask;
         }
     }
     if (real) {
-        if (p.reward) p.reward[e] = rew;
-        if (p.done) p.done[e] = died ? 1 : 0;
+        if (p.reward) p.reward[(int64_t)t * p.n + e] = rew;
+        if (p.done) p.done[(int64_t)t * p.n + e] = died ? 1 : 0;
     }
     if (F32) {
-        // float32 obs [n][W][H] of the wave's envs is one contiguous block:
-        // 16-B chunks, lane-consecutive, bits read back from L.
+        // float32 obs [n][W][H] of the wave's envs is one contiguous block,
+        // written as lane-consecutive float4 chunks.
         const int64_t nreal64 = p.n - e0 < kWave ? p.n - e0 : kWave;
         const int nreal = (int)nreal64;
-        const int per_env = W * H;
-        const int total = nreal * per_env;
-        float *out = p.obs_f32 + e0 * per_env;
-        auto word = [&](int ee, int x) { return L[(x + kPad) * kWave + ee] & hmask; };
-        if ((per_env & 3) == 0) {
-            float4 *out4 = reinterpret_cast<float4 *>(out);
-            for (int c = lane; c < total / 4; c += kWave) {
-                const int f = c * 4;
-                const int ee = f / per_env;
-                const int rem = f - ee * per_env;
-                const int x = rem / H;
-                const int y = rem - x * H;
-                float4 v;
-                if (y + 4 <= H) {
-                    const uint32_t w = word(ee, x) >> y;
-                    v.x = (float)(w & 1u);
-                    v.y = (float)((w >> 1) & 1u);
-                    v.z = (float)((w >> 2) & 1u);
-                    v.w = (float)((w >> 3) & 1u);
-                } else {
-                    float t4[4];
-                    int xx = x, yy = y;
+        float *out = p.obs_f32 + ((int64_t)t * p.n + e0) * (W * H);
+        if constexpr (WT != 0 && HT % 4 == 0) {
+            // chunk c = (env, column x, nibble q): 4 floats = bits 4q..4q+3 of
+            // the column word; the float4 comes from the 16-entry table.
+            constexpr int CPC = HT / 4, CPE = WT * CPC;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        t4[q] = (float)((word(ee, xx) >> yy) & 1u);
-                        if (++yy == H) {
-                            yy = 0;
-                            ++xx;
-                        }
-                    }
-                    v = make_float4(t4[0], t4[1], t4[2], t4[3]);
-                }
-                out4[c] = v;
+            for (int x = 0; x < WT; ++x) O[lane * (WT + 1) + x] = lcol(L, x, lane) & hmask;
+            __syncthreads();
+            float4 *out4 = reinterpret_cast<float4 *>(out);
+            const int total = nreal * CPE;
+            for (int c = lane; c < total; c += kWave) {
+                const int ee = c / CPE;
+                const int cr = c - ee * CPE;
+                const int x = cr / CPC;
+                const int q = cr - x * CPC;
+                out4[c] = F4[(O[ee * (WT + 1) + x] >> (4 * q)) & 15u];
             }
         } else {
+            const int per_env = W * H;
+            const int total = nreal * per_env;
+            auto word = [&](int ee, int x) { return L[(x + kPad) * kWave + ee] & hmask; };
             for (int f = lane; f < total; f += kWave) {
                 const int ee = f / per_env;
                 const int rem = f - ee * per_env;
@@ -689,32 +861,31 @@ __global__ __launch_bounds__(kWave) void k_step(KParams p) {
     // non-locking lanes and spawns (overlay cells were empty), and a death
     // without auto-reset (R8: _set_piece(False), tetris_env.py:303).
     __syncthreads();
-    erase(L, lane, odesc, oax, oay, hmask);
+    erase(L, lane, odesc.x, odesc.y, oax, oay, hmask);
     if (reset_now)
         for (int x = 0; x < W; ++x) lcol(L, x, lane) = floorb;
+    }  // for t
     __syncthreads();
+    uint32_t *bdst = p.board + e0;
+    uint32_t *sdst = reinterpret_cast<uint32_t *>(p.stats) + e0;
 #pragma unroll
     for (int q = 0; q < NBQ; ++q) {
-        const int i = q * kWave + lane, x = i >> 4, c = i & 15;
-        if (x < W) {
-            uint4 v = *reinterpret_cast<const uint4 *>(&L[(x + kPad) * kWave + 4 * c]);
+        if (WT || 4 * q < W) {  // rows >= W: padding rows of the allocation
+            uint4 v = *reinterpret_cast<const uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]);
             v.x &= hmask;
             v.y &= hmask;
             v.z &= hmask;
             v.w &= hmask;
-            *reinterpret_cast<uint4 *>(p.board + x * sd + e0 + 4 * c) = v;
+            *reinterpret_cast<uint4 *>(bdst + (size_t)(4 * q) * sd + loff) = v;
         }
     }
 #pragma unroll
     for (int q = 0; q < kHotQ; ++q) {
-        const int i = q * kWave + lane, r = i >> 4, c = i & 15;
-        if (r < kHotRows) {
-            uint32_t *row = r < kStatRows ? reinterpret_cast<uint32_t *>(p.stats) + r * sd : p.piece;
-            *reinterpret_cast<uint4 *>(row + e0 + 4 * c) =
-                *reinterpret_cast<const uint4 *>(&SS[r * kWave + 4 * c]);
-        }
+        if (4 * q + lrow < kHotRows)  // row 15 (ep_time) may have been stored per lane
+            *reinterpret_cast<uint4 *>(sdst + (size_t)(4 * q) * sd + loff) =
+                *reinterpret_cast<const uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]);
     }
-    if constexpr (STAMP) {
+    if constexpr (STAMP && KSTEPS == 1) {
         ST_STAMP(6);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         ST_STAMP(7);
@@ -723,6 +894,16 @@ __global__ __launch_bounds__(kWave) void k_step(KParams p) {
             for (int i = 0; i < 8; ++i) p.stamps[blockIdx.x * 8 + i] = tstamp[i];
         }
     }
+}
+
+template <int WT, int HT, bool F32, bool STAMP = false>
+__global__ __launch_bounds__(kWave) void k_step(KParams p) {
+    run_steps<WT, HT, F32, STAMP, 1>(p);
+}
+
+template <int WT, int HT, bool F32>
+__global__ __launch_bounds__(kWave) void k_rollout(KParams p) {
+    run_steps<WT, HT, F32, false, 0>(p);
 }
 
 // ---------------------------------------------------------------- reset
@@ -830,8 +1011,8 @@ __global__ __launch_bounds__(kWave) void k_render(KParams p) {
         L[(W + kPad + x) * kWave + lane] = 0u;
     }
     const uint32_t pw = p.piece[e];
-    const uint32_t d = c_tab[(pw & 7u) * 4 + ((pw >> 3) & 3u)];
-    paint(L, lane, d, (int)((pw >> 5) & 63u), (int)((pw >> 11) & 63u), hmask);
+    const uint32_t t = (pw & 7u) * 4 + ((pw >> 3) & 3u);
+    paint(L, lane, c_tab_m[t], c_tab_g[t], (int)((pw >> 5) & 63u), (int)((pw >> 11) & 63u), hmask);
     if (e < p.n)
         for (int x = 0; x < W; ++x) p.obs[x * p.n + e] = lcol(L, x, lane) & hmask;
 }
@@ -932,6 +1113,19 @@ hipError_t launch_step(const KParams &p, hipStream_t s) {
 
 hipError_t launch_render(const KParams &p, hipStream_t s) {
     hipLaunchKernelGGL(k_render, dim3((unsigned)(p.stride / kWave)), dim3(kWave), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_rollout(const KParams &p, hipStream_t s) {
+    const dim3 grid((unsigned)(p.stride / kWave)), block(kWave);
+    const bool f32 = p.obs_f32 != nullptr;
+    if (p.W == 10 && p.H == 20) {
+        if (f32) hipLaunchKernelGGL((k_rollout<10, 20, true>), grid, block, 0, s, p);
+        else hipLaunchKernelGGL((k_rollout<10, 20, false>), grid, block, 0, s, p);
+    } else {
+        if (f32) hipLaunchKernelGGL((k_rollout<0, 0, true>), grid, block, 0, s, p);
+        else hipLaunchKernelGGL((k_rollout<0, 0, false>), grid, block, 0, s, p);
+    }
     return hipGetLastError();
 }
 

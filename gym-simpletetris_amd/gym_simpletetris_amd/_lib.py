@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsimpletetris.so")
+# ST_LIB overrides the library path (diagnostic A/B builds only).
+LIB_PATH = os.environ.get("ST_LIB") or os.path.join(_HERE, "libsimpletetris.so")
 
 ST_OK, ST_EINVAL, ST_ENOMEM, ST_EHIP, ST_ESTATE = 0, -1, -2, -3, -4
 
@@ -30,11 +31,11 @@ AUTORESET = {"none": 0, "same_step": 1}
 
 # st_stat rows
 STAT = dict(time=0, score=1, lines=2, holes=3, piece_height=4, deaths=5, count0=6, mt_index=13,
-            ep_time=14, ep_score=15, ep_lines=16, ep_holes=17)
-NSTAT = 18
+            piece=14, ep_time=15, ep_score=16, ep_lines=17, ep_holes=18)
+NSTAT = 19
 MT_N = 624
 
-EXPORTS = ("st_create", "st_destroy", "st_seed", "st_reset", "st_step", "st_step_f32",
+EXPORTS = ("st_create", "st_destroy", "st_seed", "st_reset", "st_step", "st_step_f32", "st_rollout",
            "st_obs_to_f32", "st_render", "st_grayscale", "st_state", "st_copy", "st_gen_actions", "st_debug_stamps",
            "st_last_error", "st_abi_version")
 
@@ -81,6 +82,7 @@ def load(path: str = LIB_PATH):
         "st_reset": ([vp, vp, vp], ctypes.c_int),
         "st_step": ([vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "st_step_f32": ([vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
+        "st_rollout": ([vp, i32, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "st_obs_to_f32": ([vp, vp, vp, vp], ctypes.c_int),
         "st_render": ([vp, vp, vp], ctypes.c_int),
         "st_grayscale": ([vp, vp, i32, i32, i32, vp, vp], ctypes.c_int),

@@ -157,6 +157,36 @@ class TetrisBatch:
                                     _ptr(self.reward), _ptr(self.done), s))
         return (self.obs if obs == "packed" else None), self.reward, self.done
 
+    def rollout(self, actions: torch.Tensor, obs: str = "packed", out: Optional[dict] = None):
+        """K consecutive steps in one kernel launch (st_rollout).
+
+        actions: uint8 [K, n] on the device.  Returns (obs, reward, done) with
+        a leading K dimension: packed obs int32 [K, W, n] ('packed'), float32
+        [K, n, W, H] ('f32') or None ('none'); reward int32 [K, n]; done bool
+        [K, n].  Identical to K calls of step().  `out` may supply the output
+        tensors (keys 'obs', 'obs_f32', 'reward', 'done') to reuse buffers."""
+        if actions.dtype != torch.uint8 or actions.device != self.device or actions.dim() != 2 \
+                or actions.shape[1] != self.n or not actions.is_contiguous():
+            raise ValueError(f"actions must be a contiguous uint8 [K, {self.n}] tensor on {self.device}")
+        K = int(actions.shape[0])
+        out = {} if out is None else out
+        W, H, n, dev = self.width, self.height, self.n, self.device
+
+        def buf(key, shape, dtype):
+            t = out.get(key)
+            if t is None or tuple(t.shape) != shape or t.dtype != dtype:
+                t = torch.empty(shape, dtype=dtype, device=dev)
+                out[key] = t
+            return t
+        o = buf("obs", (K, W, n), torch.int32) if obs in ("packed", "f32") else None
+        f = buf("obs_f32", (K, n, W, H), torch.float32) if obs == "f32" else None
+        r = buf("reward", (K, n), torch.int32)
+        d = buf("done", (K, n), torch.bool)
+        with torch.cuda.device(dev):
+            C.check(self._L.st_rollout(self._ctx, K, _ptr(actions), _ptr(o), _ptr(f), _ptr(r),
+                                       _ptr(d), self._stream()))
+        return (f if obs == "f32" else o), r, d
+
     # ------------------------------------------------------------ observations
     def obs_to_f32(self, packed: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Packed obs -> float32 [n][W][H] (the reference's np.float32 board)."""
@@ -213,8 +243,11 @@ class TetrisBatch:
         """Upload state arrays for the real envs (shapes as returned by
         get_state); padding envs keep their current state."""
         cur = self.state_tensors(tuple(fields))
+        # `piece` aliases stats row 14: upload it after `stats`
+        order = sorted(fields, key=lambda f: ("stats", "board", "mt", "piece").index(f))
         with torch.cuda.device(self.device):
-            for f, v in fields.items():
+            for f in order:
+                v = fields[f]
                 full = cur[f].cpu().numpy().view(np.uint32).copy()
                 v = np.asarray(v).astype(np.int64).astype(np.uint32)
                 if f == "mt":

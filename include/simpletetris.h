@@ -70,7 +70,7 @@ enum st_autoreset {
 typedef struct st_config {
     int32_t width;      /* 4..32   (TetrisEnv width=10,  tetris_env.py:344) */
     int32_t height;     /* 4..28   (TetrisEnv height=20, tetris_env.py:345) */
-    int32_t lock_delay; /* 0..32766 (tetris_env.py:356; negative acts as 0, :175) */
+    int32_t lock_delay; /* <= 32766 (tetris_env.py:356; negative acts as 0, :175) */
     uint32_t flags;     /* st_flags */
     int32_t autoreset;  /* st_autoreset */
 } st_config;
@@ -86,11 +86,12 @@ enum st_stat {
     ST_STAT_DEATHS = 5,
     ST_STAT_COUNT0 = 6,   /* shape_counts T,J,L,Z,S,I,O: rows 6..12 */
     ST_STAT_MT_INDEX = 13,/* MT19937 index (0..624) */
-    ST_STAT_EP_TIME = 14, /* terminal counters of the last finished episode */
-    ST_STAT_EP_SCORE = 15,/* (ST_AUTORESET_SAME_STEP only)                   */
-    ST_STAT_EP_LINES = 16,
-    ST_STAT_EP_HOLES = 17,
-    ST_NSTAT = 18
+    ST_STAT_PIECE = 14,   /* the piece word (uint32, = st_state_views.piece) */
+    ST_STAT_EP_TIME = 15, /* terminal counters of the last finished episode */
+    ST_STAT_EP_SCORE = 16,/* (ST_AUTORESET_SAME_STEP only)                   */
+    ST_STAT_EP_LINES = 17,
+    ST_STAT_EP_HOLES = 18,
+    ST_NSTAT = 19
 };
 
 /* Device views of the context-owned state.  `stride` (>= n_envs, multiple of
@@ -99,6 +100,7 @@ enum st_stat {
  *            (the reference's board[x, y], tetris_env.py:140, one bit-packed
  *            uint32 per board row x of the (width, height) array)
  *   piece  : uint32 [stride]  id | rot<<3 | anchor_x<<5 | anchor_y<<11 | lock<<17
+ *            (an alias of stats row ST_STAT_PIECE)
  *            id in shape_names order T,J,L,Z,S,I,O (tetris_env.py:19);
  *            rot = number of rotate_left (rotated(cclk=False)) mod 4
  *   stats  : int32 [ST_NSTAT][stride]
@@ -114,7 +116,7 @@ typedef struct st_state_views {
 } st_state_views;
 
 /* ---- lifecycle: TetrisEnv.__init__ (tetris_env.py:343-392) ---------------- */
-int st_create(st_ctx **out, const st_config *cfg, int device, int64_t n_envs);
+int st_create(st_ctx **out, const st_config *cfg, int device, int64_t n_envs); /* n_envs <= 2^24 */
 int st_destroy(st_ctx *ctx);                     /* TetrisEnv.close, :466 */
 
 /* random.seed(seed[e]) for every env (host array of n_envs uint64 seeds).
@@ -144,6 +146,16 @@ int st_step(st_ctx *ctx, const uint8_t *d_actions, uint32_t *d_obs, int32_t *d_r
  * fused into the step kernel. */
 int st_step_f32(st_ctx *ctx, const uint8_t *d_actions, uint32_t *d_obs, float *d_obs_f32,
                 int32_t *d_reward, uint8_t *d_done, st_stream stream);
+
+/* k consecutive st_step calls in ONE launch: the driver loop of README.md:43-51
+ * (`for t: obs, r, done, info = env.step(a[t])`) with all actions known up
+ * front (synthetic / replayed rollouts).  Boards and counters stay on chip
+ * between steps.  d_actions: uint8 [k][n_envs]; outputs per step at [t]
+ * (any may be NULL): d_obs uint32 [k][width][n_envs], d_obs_f32 float
+ * [k][n_envs][width][height], d_reward int32 [k][n_envs], d_done uint8
+ * [k][n_envs].  Results are identical to k calls of st_step / st_step_f32. */
+int st_rollout(st_ctx *ctx, int32_t k, const uint8_t *d_actions, uint32_t *d_obs,
+               float *d_obs_f32, int32_t *d_reward, uint8_t *d_done, st_stream stream);
 
 /* Packed obs (uint32 [width][n_envs]) -> float32 [n_envs][width][height]
  * (TetrisEnv._observation 'ram' + the float32 cast, :400 / :421-424). */

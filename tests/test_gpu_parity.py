@@ -296,3 +296,115 @@ def test_vec_env_surface():
         assert o.shape == (256, 10, 20) and r.dtype == torch.int32 and d.dtype == torch.bool
     assert info["time"].shape == (256,)
     assert int(info["deaths"].sum()) > 0
+
+
+@pytest.mark.parametrize("autoreset", ["same_step", "none"])
+@pytest.mark.parametrize("board", [(10, 20), (9, 15)])
+def test_rollout_equals_steps(autoreset, board):
+    """st_rollout(K) == K x st_step, bit-exact, outputs and final state."""
+    G = _engine()
+    W, H = board
+    n, K = 1000, 150
+    kw = dict(width=W, height=H, lock_delay=1, step_reset=True, penalise_holes_increase=True,
+              advanced_clears=True, penalise_height_increase=True)
+    a = G.TetrisBatch(n, autoreset=autoreset, seeds=[3 + e for e in range(n)], **kw)
+    b = G.TetrisBatch(n, autoreset=autoreset, seeds=[3 + e for e in range(n)], **kw)
+    a.reset()
+    b.reset()
+    acts = torch.stack([a.gen_actions(t, 11).clone() for t in range(K)])
+    for obs_mode in ("packed", "f32"):
+        ro, rr, rd = b.rollout(acts, obs=obs_mode)
+        for t in range(K):
+            so, sr, sd = a.step(acts[t], obs=obs_mode)
+            assert torch.equal(so, ro[t]), (obs_mode, t)
+            assert torch.equal(sr, rr[t]) and torch.equal(sd, rd[t]), (obs_mode, t)
+        sa, sb = a.get_state(), b.get_state()
+        for k in sa:
+            assert np.array_equal(sa[k], sb[k]), (obs_mode, k)
+
+
+def test_rollout_vs_oracle_full_size():
+    """N = 65,536, K = 32 steps in one launch vs the C oracle."""
+    G = _engine()
+    n, K, seed_a = 65536, 32, 99
+    kw = dict(width=10, height=20)
+    b = G.TetrisBatch(n, autoreset="same_step", seeds=[7 + e for e in range(n)], **kw)
+    b.reset()
+    ob = O.OracleBatch(n, [7 + e for e in range(n)], **kw)
+    ob.reset()
+    acts = O.splitmix64_actions(seed_a, 0, K, n)
+    ref = ob.rollout(acts)
+    obs, rew, done = b.rollout(torch.as_tensor(acts, device=b.device))
+    assert np.array_equal(rew.cpu().numpy(), ref["reward"])
+    assert np.array_equal(done.cpu().numpy().astype(np.uint8), ref["done"])
+    assert np.array_equal(obs.cpu().numpy().view(np.uint32).transpose(0, 2, 1), ref["obs"])
+
+
+def _untemper(y):
+    """Inverse of MT19937 tempering (so crafted state words produce chosen outputs)."""
+    def undo_r(y, s):
+        x = y
+        for _ in range(32 // s + 1):
+            x = y ^ (x >> s)
+        return x & 0xFFFFFFFF
+
+    def undo_l(y, s, m):
+        x = y
+        for _ in range(32 // s + 1):
+            x = y ^ ((x << s) & m)
+        return x & 0xFFFFFFFF
+    y = undo_r(y, 18)
+    y = undo_l(y, 15, 0xEFC60000)
+    y = undo_l(y, 7, 0x9D2C5680)
+    return undo_r(y, 11)
+
+
+@pytest.mark.parametrize("mode", ["step", "rollout"])
+def test_long_rejection_runs_and_twists(mode):
+    """Crafted MT states: draws that reject 20 words in a row (past the
+    8-word prefetch and the 16-word ring), and states 1-3 words from a twist,
+    against the oracle with the same states."""
+    G = _engine()
+    n, T = 64, 40
+    b = G.TetrisBatch(n, autoreset="same_step", seeds=range(n))
+    b.reset()
+    ob = O.OracleBatch(n, list(range(n)))
+    ob.reset()
+    st = b.get_state(("mt", "stats"))
+    mt, stats = st["mt"].copy(), st["stats"].copy()
+    rej, acc = _untemper(0xFFFFFFFF), _untemper(0)
+    for i in range(n):
+        idx = int(stats[13, i])
+        if i % 4 == 0 and idx + 21 <= 624:          # 20 rejections, then accept
+            mt[i, idx:idx + 20] = rej
+            mt[i, idx + 20] = acc
+        elif i % 4 == 1:                             # next draws cross the twist
+            idx = 621 + (i % 3)
+            stats[13, i] = idx
+        elif i % 4 == 2 and idx + 41 <= 624:         # two long runs back to back
+            mt[i, idx:idx + 18] = rej
+            mt[i, idx + 18] = acc
+            mt[i, idx + 19:idx + 40] = rej
+            mt[i, idx + 40] = acc
+        e = ob.envs[i]
+        for k in range(624):
+            e.rng.mt[k] = int(mt[i, k])
+        e.rng.index = int(stats[13, i])
+    b.set_state(mt=mt, stats=stats)
+    acts = np.full((T, n), 2, np.uint8)              # hard drops: a lock every step
+    acts[::3] = O.splitmix64_actions(5, 0, T, n)[::3]
+    ref = ob.rollout(acts)
+    if mode == "step":
+        for t in range(T):
+            obs, rew, done = b.step(torch.as_tensor(acts[t], device=b.device))
+            assert np.array_equal(rew.cpu().numpy(), ref["reward"][t]), t
+            assert np.array_equal(obs.cpu().numpy().view(np.uint32).T, ref["obs"][t]), t
+    else:
+        obs, rew, done = b.rollout(torch.as_tensor(acts, device=b.device))
+        assert np.array_equal(rew.cpu().numpy(), ref["reward"])
+        assert np.array_equal(done.cpu().numpy().astype(np.uint8), ref["done"])
+        assert np.array_equal(obs.cpu().numpy().view(np.uint32).transpose(0, 2, 1), ref["obs"])
+    fin = b.get_state(("mt", "stats"))
+    for i in range(n):
+        assert int(fin["stats"][13, i]) == ob.envs[i].rng.index, i
+        assert np.array_equal(fin["mt"][i], np.ctypeslib.as_array(ob.envs[i].rng.mt)), i

@@ -13,9 +13,8 @@ timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu_$T
  && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 \
  && echo "smoke ok" \
  && timeout -k 10 600 python bench.py --steps 1000 --warmup 100 --cpu-seconds 10 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err \
- && echo "bench ok" && cat gpurun_out/bench_$TAG.json \
- && timeout -k 10 600 python bench.py --steps 1000 --warmup 100 --obs f32 --no-cpu-baseline > gpurun_out/bench_f32_$TAG.json 2>> gpurun_out/bench_$TAG.err \
- && echo "bench f32 ok" && cat gpurun_out/bench_f32_$TAG.json
+ && echo "bench ok" && cat gpurun_out/bench_$TAG.json
+
 
 rc=$?
 tail -5 gpurun_out/pytest_gpu_$TAG.log
