@@ -35,6 +35,10 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+try:
+    METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+except Exception:  # noqa: BLE001
+    METRIC = "env-steps/sec at 65 536 parallel 10\u00d720 boards; 1\u21928 GPU scaling"
 
 CONFIGS = {
     # BASELINE.json configs[2] / [3]
@@ -114,6 +118,7 @@ def main():
     ap.add_argument("--obs", choices=("packed", "f32"), default="packed")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a hipGraph")
     ap.add_argument("--gather", action="store_true", help="also time a per-step RCCL gather")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--rollout-chunk", type=int, default=100, help="steps per st_rollout launch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -126,11 +131,17 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # ST_BENCH_SHARED_GPU=1 (tests only): every rank on cuda:0, to exercise the
+    # N>1 logic on a one-GPU box with --backend gloo
+    dev_idx = 0 if os.environ.get("ST_BENCH_SHARED_GPU") == "1" else local_rank
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
 
     from gym_simpletetris_amd.distributed import ShardedTetris
 
@@ -243,7 +254,7 @@ def main():
     event_ms = ev_ms / K
     kname = f"k_step<10, 20, {'true' if f32 else 'false'}, false>"
     out = {
-        "metric": "env-steps/sec at 65 536 parallel 10x20 boards per GPU (1->8 GPU weak scaling)",
+        "metric": METRIC,
         "value": value,
         "unit": "env-steps/s",
         "n_gpus": world,
@@ -322,7 +333,7 @@ def main():
                 with torch.cuda.stream(s):
                     step(WU + i, sp)
                 s.synchronize()
-                sh.gather()
+                sh.gather(cpu=args.backend != "nccl")
             torch.cuda.synchronize(dev)
             dist.barrier()
             gdt = time.perf_counter() - g0

@@ -91,5 +91,7 @@ class ShardedTetris:
                                  ctypes.c_void_p(self._done.data_ptr()), e._stream()))
         return self._obs, self._rew, self._done
 
-    def gather(self, dst: int = 0):
-        return gather_outputs(self.buf, dst=dst)
+    def gather(self, dst: int = 0, cpu: bool = False):
+        """RCCL gather of the packed outputs to `dst` (cpu=True: via host
+        memory, for the gloo backend in tests)."""
+        return gather_outputs(self.buf.cpu() if cpu else self.buf, dst=dst)
