@@ -408,3 +408,54 @@ def test_long_rejection_runs_and_twists(mode):
     for i in range(n):
         assert int(fin["stats"][13, i]) == ob.envs[i].rng.index, i
         assert np.array_equal(fin["mt"][i], np.ctypeslib.as_array(ob.envs[i].rng.mt)), i
+
+
+def test_abi_error_paths():
+    """The C ABI rejects bad arguments and call-order violations with codes
+    and a message instead of faulting (reference: exceptions)."""
+    import ctypes
+    from gym_simpletetris_amd import _lib as C
+    L = C.load()
+    ctx = ctypes.c_void_p()
+    for cfg, n in [(C.Config(3, 20, 0, 0, 0), 8), (C.Config(10, 29, 0, 0, 0), 8),
+                   (C.Config(10, 20, 0, 1 << 9, 0), 8), (C.Config(10, 20, 0, 0, 7), 8),
+                   (C.Config(10, 20, 40000, 0, 0), 8), (C.Config(10, 20, 0, 0, 0), 0),
+                   (C.Config(10, 20, 0, 0, 0), (1 << 24) + 1)]:
+        assert L.st_create(ctypes.byref(ctx), ctypes.byref(cfg), 0, n) == C.ST_EINVAL
+        assert L.st_last_error()
+    assert L.st_create(ctypes.byref(ctx), ctypes.byref(C.Config(10, 20, 0, 0, 0)), 99, 8) == C.ST_EINVAL
+    assert L.st_create(ctypes.byref(ctx), ctypes.byref(C.Config(10, 20, 0, 0, 0)), 0, 8) == C.ST_OK
+    d = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    p = ctypes.c_void_p(d.data_ptr())
+    assert L.st_step(ctx, p, None, None, None, None) == C.ST_ESTATE      # before seed/reset
+    assert L.st_reset(ctx, None, None) == C.ST_ESTATE                    # before seed
+    assert L.st_rollout(ctx, 4, p, None, None, None, None, None) == C.ST_ESTATE
+    seeds = np.arange(8, dtype=np.uint64)
+    assert L.st_seed(ctx, ctypes.c_void_p(seeds.ctypes.data), None) == C.ST_OK
+    assert L.st_step(ctx, p, None, None, None, None) == C.ST_ESTATE      # before reset
+    assert L.st_reset(ctx, None, None) == C.ST_OK
+    assert L.st_step(ctx, None, None, None, None, None) == C.ST_EINVAL
+    assert L.st_rollout(ctx, 0, p, None, None, None, None, None) == C.ST_EINVAL
+    assert L.st_step(ctx, p, None, None, None, None) == C.ST_OK          # all outputs optional
+    assert L.st_grayscale(ctx, p, 84, 2, 0, p, None) == C.ST_EINVAL
+    assert L.st_grayscale(ctx, p, 12, 1, 0, p, None) == C.ST_EINVAL
+    assert L.st_copy(None, p, 4, None) == C.ST_EINVAL
+    torch.cuda.synchronize()
+    assert L.st_destroy(ctx) == C.ST_OK
+    assert L.st_destroy(None) == C.ST_OK
+
+
+def test_wrapper_validation():
+    G = _engine()
+    b = G.TetrisBatch(10, seeds=range(10))
+    with pytest.raises(RuntimeError):
+        G.TetrisBatch(10).reset()                  # reset before seed
+    with pytest.raises(ValueError):
+        b.seed(range(9))
+    b.reset()
+    with pytest.raises(ValueError):
+        b.step(np.zeros(9, np.uint8))
+    with pytest.raises(ValueError):
+        b.rollout(torch.zeros((3, 9), dtype=torch.uint8, device=b.device))
+    with pytest.raises(ValueError):
+        G.TetrisBatch(4, autoreset="sometimes")
