@@ -13,6 +13,7 @@ struct st_ctx {
     st_config cfg;
     uint32_t ablate;
     uint64_t *stamps;
+    uint32_t *sink;
     int device;
     int64_t n;
     int64_t stride;
@@ -75,6 +76,7 @@ st::KParams params(const st_ctx *c) {
     p.piece = c->piece;
     p.stats = c->stats;
     p.mt = c->mt;
+    p.sink = c->sink;
     return p;
 }
 
@@ -83,7 +85,9 @@ void free_state(st_ctx *c) {
     if (c->stats) (void)hipFree(c->stats);
     if (c->mt) (void)hipFree(c->mt);
     if (c->stamps) (void)hipFree(c->stamps);
+    if (c->sink) (void)hipFree(c->sink);
     c->stamps = nullptr;
+    c->sink = nullptr;
     c->board = c->piece = c->mt = nullptr;
     c->stats = nullptr;
 }
@@ -129,8 +133,9 @@ int st_create(st_ctx **out, const st_config *cfg, int device, int64_t n_envs) {
     if (e == hipSuccess) e = hipMalloc(&c->stats, sd * ST_NSTAT * sizeof(int32_t));
     if (e == hipSuccess) c->piece = reinterpret_cast<uint32_t *>(c->stats) + ST_STAT_PIECE * sd;
     if (e == hipSuccess) e = hipMalloc(&c->mt, sd * st::kMtN * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&c->sink, 128 * sizeof(uint32_t));
     if (e == hipSuccess && getenv("ST_STAMPS"))
-        e = hipMalloc(&c->stamps, (sd / st::kWave) * 8 * sizeof(uint64_t));
+        e = hipMalloc(&c->stamps, (sd / st::kWave) * st::kStampWords * sizeof(uint64_t));
     if (e != hipSuccess) {
         free_state(c);
         delete c;
@@ -281,7 +286,7 @@ int st_debug_stamps(st_ctx *c, uint64_t *host_out, int64_t max_words) {
     if (!c || !host_out) return fail(ST_EINVAL, "st_debug_stamps: null argument");
     if (!c->stamps) return fail(ST_ESTATE, "context was not created with ST_STAMPS set");
     DeviceGuard g(c->device);
-    int64_t n = (c->stride / st::kWave) * 8;
+    int64_t n = (c->stride / st::kWave) * st::kStampWords;
     if (max_words < n) n = max_words;
     ST_HIP(hipDeviceSynchronize());
     ST_HIP(hipMemcpy(host_out, c->stamps, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost));

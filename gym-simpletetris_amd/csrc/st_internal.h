@@ -12,6 +12,9 @@ constexpr int kPad = 4;        // wall columns on each side of the LDS board
 constexpr int kMaxW = 32;
 constexpr int kMaxH = 28;
 constexpr int kMtN = 624;
+// diagnostic stamps per wave: 8 s_memtime phase stamps, s_memrealtime at
+// start and end, HW_ID, XCC_ID
+constexpr int kStampWords = 12;
 constexpr int kPieceRow = ST_STAT_PIECE;     // rows 0..14 (counters + piece) move every step
 constexpr int kHotRows = ST_STAT_PIECE + 1;
 constexpr int kHotQ = (kHotRows * 16 + kWave - 1) / kWave;  // 16-B slots per lane
@@ -42,6 +45,8 @@ struct KParams {
     float *obs_f32;          // [n][W][H]
     int32_t *reward;         // [n]
     uint8_t *done;           // [n]
+    uint32_t *sink;          // [128] store target of masked-off lanes (keeps the
+                             // step's early stores branch-free, see run_steps)
 };
 
 hipError_t launch_seed(const KParams &p, hipStream_t s);

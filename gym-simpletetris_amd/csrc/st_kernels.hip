@@ -176,13 +176,6 @@ __device__ __forceinline__ uint32_t compact(uint32_t v, uint32_t full) {
     return v;
 }
 
-// _count_holes (tetris_env.py:218-220) for one column: empty cells below the
-// topmost filled cell.
-__device__ __forceinline__ int col_holes(uint32_t v, uint32_t hmask) {
-    const uint32_t above = (v & (0u - v)) - 1u;  // rows above the topmost cell (all if v == 0)
-    return __builtin_popcount(hmask & ~(v | above));
-}
-
 // ---------------------------------------------------------------- MT19937
 // CPython Modules/_randommodule.c genrand_uint32 / init_by_array.
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
@@ -269,9 +262,14 @@ __device__ void coop_twist(uint32_t *g, uint32_t *S, int lane) {
 // the lock-path work).
 __device__ __forceinline__ void prefetch_words(const uint32_t *g, int32_t mtidx, bool want,
                                                uint32_t (&w)[8]) {
+    // one exec region; indices clamped (words past the state are never consumed)
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-        w[j] = (want && mtidx + j < kMtN) ? __builtin_nontemporal_load(g + mtidx + j) : 0u;
+    for (int j = 0; j < 8; ++j) w[j] = 0u;
+    if (want) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            w[j] = __builtin_nontemporal_load(g + (mtidx + j < kMtN ? mtidx + j : kMtN - 1));
+    }
 }
 
 __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], int32_t &mtidx,
@@ -289,17 +287,13 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], int32_t 
     bool pending = need;
     bool fresh = false;  // state twisted (and stored) by this wave in this launch
     uint32_t r = 0;
+    uint32_t w[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = pre[j];
+    bool have = have_pre && pending && mtidx < kMtN;  // first round: words prefetched by the caller
     while (__ballot(pending)) {
         if (!twist && pending && mtidx >= kMtN) mtidx = 0;  // ablation: skip the twist
         uint64_t tw = __ballot(pending && mtidx >= kMtN);
-        uint32_t w[8];
-        bool have = false;
-        if (have_pre && pending && mtidx < kMtN) {  // words prefetched by the caller
-#pragma unroll
-            for (int j = 0; j < 8; ++j) w[j] = pre[j];
-            have = true;
-        }
-        have_pre = false;
         if (tw) {
             bool mine = false;  // this lane's state was twisted in this round
             do {
@@ -326,7 +320,7 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], int32_t 
             if (__ballot(pending && fresh)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-                w[j] = (mtidx + j < kMtN) ? __builtin_nontemporal_load(g + mtidx + j) : 0u;
+                w[j] = __builtin_nontemporal_load(g + (mtidx + j < kMtN ? mtidx + j : kMtN - 1));
         }
         // consume words until every lane has its piece (most waves stop after
         // 3-5 of the 8: each getrandbits(k) is accepted with p >= 1/2)
@@ -342,6 +336,7 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], int32_t 
                 }
             }
         }
+        have = false;
     }
     if (!need) return 0;
     int32_t rr = (int32_t)r + 1;
@@ -536,6 +531,8 @@ __device__ __forceinline__ uint32_t pack_piece(int id, int rot, int ax, int ay, 
 template <int WT, int HT, bool F32, bool STAMP, int KSTEPS>
 __device__ __forceinline__ void run_steps(const KParams &p) {
     [[maybe_unused]] uint64_t tstamp[8] = {};
+    [[maybe_unused]] uint64_t rt0 = 0;
+    if constexpr (STAMP) rt0 = __builtin_amdgcn_s_memrealtime();
     ST_STAMP(0);
     // LDS: board columns L[x + kPad][lane] (walls at both ends), the staged
     // counter rows SS[r][lane] (r < 14: stats rows, 14: piece word), the MT
@@ -544,6 +541,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     __shared__ __attribute__((aligned(16))) uint32_t SS[kHotQ * 4 * kWave];
     __shared__ uint32_t S[kMtN];
     __shared__ uint2 T2[28];
+    __shared__ __attribute__((aligned(16))) uint32_t KM[KSTEPS == 1 ? kWave : 4];  // st_step: board keep-mask per env
     // float32 obs writer (F32): per-lane obs words at stride W+1 (conflict-
     // free transposed reads) and the 16 float4 patterns of a 4-bit nibble.
     __shared__ uint32_t O[F32 ? kWave * (kMaxW + 1) : 1];
@@ -638,15 +636,16 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     uint32_t cur[4], cand[4];
     read_cols(L, lane, desc.y, ax, cur);
     read_cols(L, lane, cdesc.y, cx, cand);
-    int d;
-    if (tries && !collides_v(cdesc.x, ay, cand)) {
-        ax = cx;
-        rot = cr;
-        desc = cdesc;
-        d = drop_v(cdesc.y, ay, cand);
-    } else {
-        d = drop_v(desc.y, ay, cur);
-    }
+    // branch-free: select the accepted position's descriptor and columns, then
+    // one drop test (both arms would otherwise run in a divergent wave)
+    const bool ok = tries && !collides_v(cdesc.x, ay, cand);
+    ax = ok ? cx : ax;
+    rot = ok ? cr : rot;
+    desc.x = ok ? cdesc.x : desc.x;
+    desc.y = ok ? cdesc.y : desc.y;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cur[j] = ok ? cand[j] : cur[j];
+    int d = drop_v(desc.y, ay, cur);
     if (act == 2u) {                 // hard_drop :54-59
         ay += d;
         d = 0;
@@ -664,7 +663,8 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     int32_t rew = (p.flags & ST_REWARD_STEP) ? 1 : 0;
     bool locknow = false;
     if (d == 0) {
-        lock = lock + 1 < p.lock_mod ? lock + 1 : (p.lock_mod == 1 ? 0 : (lock + 1) % p.lock_mod);
+        const int l1 = lock + 1;  // (x + 1) % lock_mod; x < lock_mod unless set_state said otherwise
+        lock = l1 < p.lock_mod ? l1 : (l1 == p.lock_mod ? 0 : l1 % p.lock_mod);
         locknow = lock == 0 && !(p.ablate & 1u);
     }
     ST_STAMP(2);
@@ -685,31 +685,41 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         height = (int32_t)ss(ST_STAT_PIECE_HEIGHT);
         deaths = (int32_t)ss(ST_STAT_DEATHS);
         paint(L, lane, desc.x, desc.y, ax, ay, hmask);
-        uint32_t andv = hmask, orv = 0;
-        int32_t nh = 0;
+        // Column words carry the floor bits, so the topmost cell of column v
+        // is ctz(v) (H when empty) and its holes are H - ctz(v) - popc(v & hmask):
+        // summed, holes = W*H - sum ctz(v) - (sum popc(v) - W*(32-H)).
+        uint32_t andv = ~0u, orv = 0, sctz = 0, spop = 0;
 #pragma unroll 8
         for (int x = 0; x < W; ++x) {
-            const uint32_t v = lcol(L, x, lane) & hmask;
+            const uint32_t v = lcol(L, x, lane);
             andv &= v;
             orv |= v;
-            nh += col_holes(v, hmask);
+            sctz += __builtin_ctz(v);
+            spop += __builtin_popcount(v);
         }
+        andv &= hmask;
         int32_t ncl = 0;
         if (andv) {  // full rows: compact, recount
             ncl = __builtin_popcount(andv);
             orv = 0;
-            nh = 0;
+            sctz = spop = 0;
 #pragma unroll 8
             for (int x = 0; x < W; ++x) {
-                const uint32_t v = compact(lcol(L, x, lane) & hmask, andv);
-                lcol(L, x, lane) = v | floorb;
+                const uint32_t v = compact(lcol(L, x, lane) & hmask, andv) | floorb;
+                lcol(L, x, lane) = v;
                 orv |= v;
-                nh += col_holes(v, hmask);
+                sctz += __builtin_ctz(v);
+                spop += __builtin_popcount(v);
             }
             lines += ncl;
         }
+        orv &= hmask;
+        const int32_t nh = W * H - (int32_t)sctz - ((int32_t)spop - W * (32 - H));
         if (p.flags & ST_ADVANCED_CLEARS) {  // :266-269, 2.5 * [0,40,100,300,1200]
-            const int32_t sc = ncl == 1 ? 40 : ncl == 2 ? 100 : ncl == 3 ? 300 : ncl == 4 ? 1200 : 0;
+            // [0, 40, 100, 300, 1200][ncl] as 12-bit fields of one constant
+            // (ncl > 4 only from a crafted set_state board: 0, as before)
+            constexpr uint64_t kClr = (40ull << 12) | (100ull << 24) | (300ull << 36) | (1200ull << 48);
+            const int32_t sc = ncl <= 4 ? (int32_t)((kClr >> (12 * ncl)) & 0xFFFu) : 0;
             rew += (sc * 5) / 2;
             score += sc;
         } else if (p.flags & ST_HIGH_SCORING) {  // :270-272
@@ -741,12 +751,56 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     }
     ST_STAMP(3);
 
-    // ---- spawn (:299 _new_piece) or same-step reset (:306-315) ----
     const bool reset_now = died && p.autoreset == ST_AUTORESET_SAME_STEP;
     const bool draw = spawn || reset_now;
+    // reward / done never depend on the piece drawn below.  Stored without
+    // a branch (masked-off lanes and absent outputs write the sink): vmcnt
+    // counts loads and stores in issue order, and a store skipped on some
+    // path would make the MT-word wait in the draw a full vmcnt(0).
+    auto store_rd = [&]() {
+        const int64_t o = (int64_t)t * p.n + e;
+        int32_t *rp = (p.reward && real) ? p.reward + o : reinterpret_cast<int32_t *>(p.sink) + lane;
+        uint8_t *dp = (p.done && real) ? p.done + o : reinterpret_cast<uint8_t *>(p.sink + 64) + lane;
+        *rp = rew;
+        *dp = died ? 1 : 0;
+    };
+    store_rd();
+    if constexpr (KSTEPS == 1) {
+        // The post-step board never depends on the drawn piece either (a spawn
+        // only overlays row 0, which is empty after a non-fatal lock, :277), so
+        // st_step stores it here and the stores drain under the MT-word wait:
+        // non-locking lanes and spawns: L; a death without auto-reset: L minus
+        // the locked piece (R8: _set_piece(False), :303); a same-step reset:
+        // the empty board.  The obs overlay of every non-spawning lane is then
+        // painted (a death's terminal obs = L with its piece, :301).
+        if (died && !reset_now) erase(L, lane, desc.x, desc.y, ax, ay, hmask);
+        KM[lane] = reset_now ? 0u : hmask;
+        __syncthreads();
+        const uint4 km = *reinterpret_cast<const uint4 *>(&KM[lcc]);
+        uint4 bw[NBQ];
+#pragma unroll
+        for (int q = 0; q < NBQ; ++q)
+            if (WT || 4 * q < W) bw[q] = *reinterpret_cast<const uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]);
+        uint32_t *bdst = p.board + e0;
+#pragma unroll
+        for (int q = 0; q < NBQ; ++q) {
+            if (WT || 4 * q < W) {  // rows >= W: padding rows of the allocation
+                uint4 v = bw[q];
+                v.x &= km.x;
+                v.y &= km.y;
+                v.z &= km.z;
+                v.w &= km.w;
+                *reinterpret_cast<uint4 *>(bdst + (size_t)(4 * q) * sd + loff) = v;
+            }
+        }
+        __syncthreads();  // the board reads above precede the overlay paint
+        if (!spawn) paint(L, lane, desc.x, desc.y, ax, ay, hmask);
+    }
+
+    // ---- spawn (:299 _new_piece) or same-step reset (:306-315) ----
     int32_t cnt[7];
 #pragma unroll
-    for (int i = 0; i < 7; ++i) cnt[i] = draw ? (int32_t)ss(ST_STAT_COUNT0 + i) : 0;
+    for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)ss(ST_STAT_COUNT0 + i);  // used by drawing lanes only
     int pick = 0;
     if (!(p.ablate & 2u)) {
         if constexpr (!kRing) {
@@ -770,7 +824,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     }
 
     // ---- counters back to the staged rows (tetris_env.py:253, :264-299) ----
-    if (reset_now) {
+    if (reset_now) {  // the finished episode's counters (ST_AUTORESET_SAME_STEP)
         int32_t *st = p.stats + e;
         st[ST_STAT_EP_TIME * sd] = time;
         st[ST_STAT_EP_SCORE * sd] = score;
@@ -787,11 +841,11 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         ss(ST_STAT_PIECE_HEIGHT) = (uint32_t)height;
         ss(ST_STAT_DEATHS) = (uint32_t)deaths;
         ss(ST_STAT_MT_INDEX) = (uint32_t)mtidx;
-        if (draw) ss(ST_STAT_COUNT0 + pick) += 1u;  // shape_counts[name] += 1, :199
+        if (draw) atomicAdd(&ss(ST_STAT_COUNT0 + pick), 1u);  // shape_counts[name] += 1, :199 (ds_add, no return)
     }
 
     // ---- observation (tetris_env.py:301-302): board + current piece ----
-    paint(L, lane, odesc.x, odesc.y, oax, oay, hmask);
+    if (KSTEPS != 1 || spawn) paint(L, lane, odesc.x, odesc.y, oax, oay, hmask);
     __syncthreads();
     const bool wide_obs = (p.n & 3) == 0 && e0 + kWave <= p.n &&
                           (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0;
@@ -800,7 +854,8 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
             const uint32_t noff = (uint32_t)lrow * (uint32_t)p.n + (uint32_t)lcc;
             uint32_t *odst = obs_t + e0;
 #pragma unroll
-            for (int q = 0; q < NBQ; ++q) {
+            for (int q = 0; q < NBQ; ++q) {  // interleaved read/store (measured: reads-first
+                                             // costs the packed rollout ~7%)
                 if ((WT || 4 * q < W) && 4 * q + lrow < W) {
                     uint4 v = *reinterpret_cast<const uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]);
                     v.x &= hmask;
@@ -813,10 +868,6 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         } else if (real) {
             for (int x = 0; x < W; ++x) obs_t[x * p.n + e] = lcol(L, x, lane) & hmask;
         }
-    }
-    if (real) {
-        if (p.reward) p.reward[(int64_t)t * p.n + e] = rew;
-        if (p.done) p.done[(int64_t)t * p.n + e] = died ? 1 : 0;
     }
     if (F32) {
         // float32 obs [n][W][H] of the wave's envs is one contiguous block,
@@ -855,30 +906,33 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     }
     ST_STAMP(5);
 
-    // ---- state: board = obs minus the overlay (no-op where the overlay was
-    // already part of the board... see below), counters, piece ----
-    // Erasing the overlaid piece yields the post-step board for every lane:
-    // non-locking lanes and spawns (overlay cells were empty), and a death
-    // without auto-reset (R8: _set_piece(False), tetris_env.py:303).
-    __syncthreads();
-    erase(L, lane, odesc.x, odesc.y, oax, oay, hmask);
-    if (reset_now)
-        for (int x = 0; x < W; ++x) lcol(L, x, lane) = floorb;
+    if constexpr (KSTEPS != 1) {
+        // ---- state for the next step: board = obs minus the overlay ----
+        // Erasing the overlaid piece yields the post-step board for every
+        // lane: non-locking lanes and spawns (overlay cells were empty), and a
+        // death without auto-reset (R8: _set_piece(False), tetris_env.py:303).
+        __syncthreads();
+        erase(L, lane, odesc.x, odesc.y, oax, oay, hmask);
+        if (reset_now)
+            for (int x = 0; x < W; ++x) lcol(L, x, lane) = floorb;
+    }
     }  // for t
     __syncthreads();
-    uint32_t *bdst = p.board + e0;
-    uint32_t *sdst = reinterpret_cast<uint32_t *>(p.stats) + e0;
+    if constexpr (KSTEPS != 1) {
+        uint32_t *bdst = p.board + e0;
 #pragma unroll
-    for (int q = 0; q < NBQ; ++q) {
-        if (WT || 4 * q < W) {  // rows >= W: padding rows of the allocation
-            uint4 v = *reinterpret_cast<const uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]);
-            v.x &= hmask;
-            v.y &= hmask;
-            v.z &= hmask;
-            v.w &= hmask;
-            *reinterpret_cast<uint4 *>(bdst + (size_t)(4 * q) * sd + loff) = v;
+        for (int q = 0; q < NBQ; ++q) {
+            if (WT || 4 * q < W) {  // rows >= W: padding rows of the allocation
+                uint4 v = *reinterpret_cast<const uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]);
+                v.x &= hmask;
+                v.y &= hmask;
+                v.z &= hmask;
+                v.w &= hmask;
+                *reinterpret_cast<uint4 *>(bdst + (size_t)(4 * q) * sd + loff) = v;
+            }
         }
     }
+    uint32_t *sdst = reinterpret_cast<uint32_t *>(p.stats) + e0;
 #pragma unroll
     for (int q = 0; q < kHotQ; ++q) {
         if (4 * q + lrow < kHotRows)  // row 15 (ep_time) may have been stored per lane
@@ -891,7 +945,11 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         ST_STAMP(7);
         if (lane == 0) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) p.stamps[blockIdx.x * 8 + i] = tstamp[i];
+            for (int i = 0; i < 8; ++i) p.stamps[blockIdx.x * kStampWords + i] = tstamp[i];
+            p.stamps[blockIdx.x * kStampWords + 8] = rt0;
+            p.stamps[blockIdx.x * kStampWords + 9] = __builtin_amdgcn_s_memrealtime();
+            p.stamps[blockIdx.x * kStampWords + 10] = __builtin_amdgcn_s_getreg(0xF804);  // HW_ID
+            p.stamps[blockIdx.x * kStampWords + 11] = __builtin_amdgcn_s_getreg(0xF814);  // XCC_ID
         }
     }
 }

@@ -17,17 +17,40 @@ n = 65536
 b = G.TetrisBatch(n, autoreset="same_step", seeds=[1000 + e for e in range(n)])
 b.reset()
 nw = b.stride // 64
-buf = np.zeros(nw * 8, np.uint64)
-names = ["loads", "action+drop", "lock path", "draw", "obs+stores issue", "f32 block", "store drain"]
+W = 12  # kStampWords
+buf = np.zeros(nw * W, np.uint64)
+rts = []
+names = ["loads", "action+drop", "lock path", "draw", "obs (+f32) issue", "state stores issue", "store drain"]
 acc = []
 for t in range(300):
     b.step(b.gen_actions(t, 0x5EED), obs="f32" if f32 else "packed")
     if t >= 100:
         b._L.st_debug_stamps(b._ctx, ctypes.c_void_p(buf.ctypes.data), buf.size)
-        st = buf.reshape(nw, 8).astype(np.int64)
-        acc.append(np.diff(st, axis=1))
+        full = buf.reshape(nw, W).astype(np.int64)
+        acc.append(np.diff(full[:, :8], axis=1))
+        rts.append(full[:, 8:12].copy())
 a = np.concatenate(acc)
 tot = (a.sum(1))
 print(f"f32={f32} waves={nw} steps=200  total cycles median {np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} max {tot.max()}")
 for i, nm in enumerate(names):
     print(f"  {nm:18s} median {np.median(a[:, i]):7.0f}  mean {a[:, i].mean():7.0f}  p90 {np.percentile(a[:, i], 90):7.0f}")
+
+# wave placement in time (s_memrealtime, 100 MHz => 10 ns ticks)
+r = np.stack(rts)  # [steps, waves, 4]
+t0 = r[:, :, 0] - r[:, :, 0].min(axis=1, keepdims=True)
+t1 = r[:, :, 1] - r[:, :, 0].min(axis=1, keepdims=True)
+ns = 10.0
+print(f"wave start offset ns: median {np.median(t0)*ns:.0f} p90 {np.percentile(t0, 90)*ns:.0f} max {t0.max(1).mean()*ns:.0f} (mean over steps)")
+print(f"wave end   offset ns: median {np.median(t1)*ns:.0f} p90 {np.percentile(t1, 90)*ns:.0f} max {t1.max(1).mean()*ns:.0f}")
+print(f"wave life ns: median {np.median(t1 - t0)*ns:.0f}")
+xcc = r[0, :, 3] & 0xF
+hw = r[0, :, 2]
+cu = (hw >> 8) & 0xF
+se = (hw >> 13) & 0x7
+simd = (hw >> 4) & 0x3
+print("waves per xcc", np.bincount(xcc, minlength=8).tolist())
+print("distinct (xcc,se,cu):", len(set(zip(xcc.tolist(), se.tolist(), cu.tolist()))), " simd hist", np.bincount(simd, minlength=4).tolist())
+for k in range(8):
+    m = xcc == k
+    if m.any():
+        print(f"  xcc {k}: start median {np.median(t0[:, m])*ns:.0f} end max {t1[:, m].max(1).mean()*ns:.0f}")
