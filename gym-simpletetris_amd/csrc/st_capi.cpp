@@ -13,7 +13,6 @@ struct st_ctx {
     st_config cfg;
     uint32_t ablate;
     uint64_t *stamps;
-    uint32_t *sink;
     int device;
     int64_t n;
     int64_t stride;
@@ -76,7 +75,6 @@ st::KParams params(const st_ctx *c) {
     p.piece = c->piece;
     p.stats = c->stats;
     p.mt = c->mt;
-    p.sink = c->sink;
     return p;
 }
 
@@ -85,9 +83,7 @@ void free_state(st_ctx *c) {
     if (c->stats) (void)hipFree(c->stats);
     if (c->mt) (void)hipFree(c->mt);
     if (c->stamps) (void)hipFree(c->stamps);
-    if (c->sink) (void)hipFree(c->sink);
     c->stamps = nullptr;
-    c->sink = nullptr;
     c->board = c->piece = c->mt = nullptr;
     c->stats = nullptr;
 }
@@ -133,7 +129,6 @@ int st_create(st_ctx **out, const st_config *cfg, int device, int64_t n_envs) {
     if (e == hipSuccess) e = hipMalloc(&c->stats, sd * ST_NSTAT * sizeof(int32_t));
     if (e == hipSuccess) c->piece = reinterpret_cast<uint32_t *>(c->stats) + ST_STAT_PIECE * sd;
     if (e == hipSuccess) e = hipMalloc(&c->mt, sd * st::kMtN * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMalloc(&c->sink, 128 * sizeof(uint32_t));
     if (e == hipSuccess && getenv("ST_STAMPS"))
         e = hipMalloc(&c->stamps, (sd / st::kWave) * st::kStampWords * sizeof(uint64_t));
     if (e != hipSuccess) {

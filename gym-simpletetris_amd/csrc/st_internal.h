@@ -45,8 +45,6 @@ struct KParams {
     float *obs_f32;          // [n][W][H]
     int32_t *reward;         // [n]
     uint8_t *done;           // [n]
-    uint32_t *sink;          // [128] store target of masked-off lanes (keeps the
-                             // step's early stores branch-free, see run_steps)
 };
 
 hipError_t launch_seed(const KParams &p, hipStream_t s);

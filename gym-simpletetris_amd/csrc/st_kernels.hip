@@ -109,6 +109,21 @@ __device__ __forceinline__ uint32_t pc_bits(uint32_t m, int j, int y) {
     return (uint32_t)((uint64_t)((m >> (8 * j)) & 0xFFu) << y >> 3);
 }
 
+// Branch-free masked stores: raw buffer stores whose lanes get an offset past
+// the resource's range are dropped by the hardware (no traffic), and unlike a
+// store under `if` they keep the compiler's vmcnt bookkeeping exact (a store
+// skipped on some path turns later waits on older loads into vmcnt(0)).
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kOff = 0xFFFFFFF0u;  // "no store" offset (>= every range used)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, base ? (int)bytes : 0,
+                                             0x00020000);
+}
+__device__ __forceinline__ void buf_store16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
+    const i32x4 d = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(d, r, off, 0, 0);
+}
+
 __device__ __forceinline__ uint32_t &lcol(uint32_t *L, int x, int lane) {
     return L[(x + kPad) * kWave + lane];
 }
@@ -287,6 +302,12 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], int32_t 
     bool pending = need;
     bool fresh = false;  // state twisted (and stored) by this wave in this launch
     uint32_t r = 0;
+    // Take all 8 prefetched words here (one vmcnt(#younger ops) wait on the
+    // loop's single entry path).  Words the loop never reads would otherwise
+    // stay "pending" for the compiler, and every later reuse of their
+    // registers would wait vmcnt(0) -- draining the caller's early stores.
+    asm volatile("" ::"v"(pre[0]), "v"(pre[1]), "v"(pre[2]), "v"(pre[3]), "v"(pre[4]), "v"(pre[5]),
+                 "v"(pre[6]), "v"(pre[7]));
     uint32_t w[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) w[j] = pre[j];
@@ -321,6 +342,8 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], int32_t 
 #pragma unroll
             for (int j = 0; j < 8; ++j)
                 w[j] = __builtin_nontemporal_load(g + (mtidx + j < kMtN ? mtidx + j : kMtN - 1));
+            asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]),
+                         "v"(w[6]), "v"(w[7]));  // see above: no loads left pending
         }
         // consume words until every lane has its piece (most waves stop after
         // 3-5 of the 8: each getrandbits(k) is accepted with p >= 1/2)
@@ -541,7 +564,10 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     __shared__ __attribute__((aligned(16))) uint32_t SS[kHotQ * 4 * kWave];
     __shared__ uint32_t S[kMtN];
     __shared__ uint2 T2[28];
-    __shared__ __attribute__((aligned(16))) uint32_t KM[KSTEPS == 1 ? kWave : 4];  // st_step: board keep-mask per env
+    // st_step: per env board keep-mask, changed board columns, changed counter rows
+    __shared__ __attribute__((aligned(16))) uint32_t KM[KSTEPS == 1 ? kWave : 4];
+    __shared__ __attribute__((aligned(16))) uint32_t BD[KSTEPS == 1 ? kWave : 4];
+    __shared__ __attribute__((aligned(16))) uint32_t SD[KSTEPS == 1 ? kWave : 4];
     // float32 obs writer (F32): per-lane obs words at stride W+1 (conflict-
     // free transposed reads) and the 16 float4 patterns of a 4-bit nibble.
     __shared__ uint32_t O[F32 ? kWave * (kMaxW + 1) : 1];
@@ -567,26 +593,54 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     constexpr int NBQ = ((WT ? WT : kMaxW) + 3) / 4;  // board 4-row groups
     const uint32_t *bsrc = p.board + e0;
     const uint32_t *ssrc = reinterpret_cast<const uint32_t *>(p.stats) + e0;
+    // Rows past the last real row (board padding, counter row 15) re-read the
+    // last row -- the same cache line another lane fetches -- instead of
+    // fetching padding; the loads stay unconditional (a load under a branch
+    // costs a full vmcnt wait at the join).
+    auto clamp_off = [&](int q, int nrows) -> uint32_t {
+        const int r = 4 * q + (lane >> 4) < nrows ? (lane >> 4) : nrows - 1 - 4 * q;
+        return (uint32_t)r * (uint32_t)sd + 4u * (uint32_t)(lane & 15);
+    };
     uint4 bv[NBQ];
 #pragma unroll
     for (int q = 0; q < NBQ; ++q)
-        if (WT || 4 * q < W) bv[q] = *reinterpret_cast<const uint4 *>(bsrc + (size_t)(4 * q) * sd + loff);
+        if (WT || 4 * q < W)
+            bv[q] = *reinterpret_cast<const uint4 *>(bsrc + (size_t)(4 * q) * sd +
+                                                     (4 * q + 4 <= W ? loff : clamp_off(q, W)));
     uint4 sv[kHotQ];
 #pragma unroll
     for (int q = 0; q < kHotQ; ++q)
-        sv[q] = *reinterpret_cast<const uint4 *>(ssrc + (size_t)(4 * q) * sd + loff);
+        sv[q] = *reinterpret_cast<const uint4 *>(ssrc + (size_t)(4 * q) * sd +
+                                                 (4 * q + 4 <= kHotRows ? loff : clamp_off(q, kHotRows)));
     const int K = KSTEPS ? KSTEPS : p.k;
-    uint32_t act_next = real ? (uint32_t)p.actions[e] : 6u;
-    const uint2 tabv = make_uint2(c_tab_m[lane < 28 ? lane : 0], c_tab_g[lane < 28 ? lane : 0]);
+    // unconditional (clamped) so it is issued with the others; masked at use
+    uint32_t act_next = p.actions[real ? e : p.n - 1];
+    // The piece table, lane i = entry i, from immediates by compare/select
+    // (VALU under the load latency; no memory access: a __constant__ load
+    // gets sunk by the compiler past the state loads' completion -- one more
+    // serialized round trip -- and inline asm here makes the register
+    // allocator spill the in-flight state loads to scratch).
+#if defined(ST_AB_TAB_LOAD) && ST_AB_TAB_LOAD
+    const uint32_t tab_m = c_tab_m[lane < 28 ? lane : 0], tab_g = c_tab_g[lane < 28 ? lane : 0];
+#else
+    uint32_t tab_m = 0, tab_g = 0;
+#pragma unroll
+    for (int i = 0; i < 28; ++i) {
+        const bool me = lane == i;
+        tab_m = me ? kTab.m[i] : tab_m;
+        tab_g = me ? kTab.g[i] : tab_g;
+    }
+#endif
+    const uint32_t floor_op = floorb;
     const int lrow = lane >> 4, lcc = 4 * (lane & 15);  // this lane's row-in-group, env slot
 #pragma unroll
     for (int q = 0; q < NBQ; ++q) {
         if (WT || 4 * q < W) {
             uint4 v = bv[q];
-            v.x |= floorb;
-            v.y |= floorb;
-            v.z |= floorb;
-            v.w |= floorb;
+            v.x |= floor_op;
+            v.y |= floor_op;
+            v.z |= floor_op;
+            v.w |= floor_op;
             *reinterpret_cast<uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]) = v;
         }
     }
@@ -598,7 +652,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
 #pragma unroll
     for (int q = 0; q < kHotQ; ++q)
         *reinterpret_cast<uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]) = sv[q];
-    if (lane < 28) T2[lane] = tabv;
+    if (lane < 28) T2[lane] = make_uint2(tab_m, tab_g);
     if constexpr (F32) {
         if (lane < 16)
             F4[lane] = make_float4((float)(lane & 1), (float)((lane >> 1) & 1),
@@ -612,8 +666,8 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     if constexpr (kRing) ring_init(ring, R, p.mt + e * kMtN, (int32_t)ss(ST_STAT_MT_INDEX), lane);
 
     for (int t = 0; t < K; ++t) {
-    const uint32_t act = act_next;
-    if (KSTEPS != 1 && t + 1 < K) act_next = real ? (uint32_t)p.actions[(int64_t)(t + 1) * p.n + e] : 6u;
+    const uint32_t act = real ? act_next : 6u;
+    if (KSTEPS != 1 && t + 1 < K) act_next = p.actions[(int64_t)(t + 1) * p.n + (real ? e : p.n - 1)];
     uint32_t *const obs_t = p.obs ? p.obs + (int64_t)t * W * p.n : nullptr;
     const uint32_t pw = ss(kPieceRow);
     int32_t time = (int32_t)ss(ST_STAT_TIME);
@@ -678,6 +732,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     // ---- lock path (tetris_env.py:263-299) ----
     bool died = false, spawn = false;
     int32_t score = 0, lines = 0, holes = 0, height = 0, deaths = 0;
+    uint32_t bdirty = 0;  // st_step: board columns this step changes (stores skip the rest)
     if (locknow) {
         score = (int32_t)ss(ST_STAT_SCORE);
         lines = (int32_t)ss(ST_STAT_LINES);
@@ -698,6 +753,11 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
             spop += __builtin_popcount(v);
         }
         andv &= hmask;
+        if constexpr (KSTEPS == 1) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bdirty |= 1u << (ax + pc_dx(desc.y, j));
+            if (andv) bdirty = ~0u;
+        }
         int32_t ncl = 0;
         if (andv) {  // full rows: compact, recount
             ncl = __builtin_popcount(andv);
@@ -753,16 +813,14 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
 
     const bool reset_now = died && p.autoreset == ST_AUTORESET_SAME_STEP;
     const bool draw = spawn || reset_now;
-    // reward / done never depend on the piece drawn below.  Stored without
-    // a branch (masked-off lanes and absent outputs write the sink): vmcnt
-    // counts loads and stores in issue order, and a store skipped on some
-    // path would make the MT-word wait in the draw a full vmcnt(0).
+    // reward / done never depend on the piece drawn below.  Buffer stores
+    // (buf_rsrc): vmcnt counts loads and stores in issue order, and a store
+    // skipped on some path would make the MT-word wait in the draw vmcnt(0).
     auto store_rd = [&]() {
-        const int64_t o = (int64_t)t * p.n + e;
-        int32_t *rp = (p.reward && real) ? p.reward + o : reinterpret_cast<int32_t *>(p.sink) + lane;
-        uint8_t *dp = (p.done && real) ? p.done + o : reinterpret_cast<uint8_t *>(p.sink + 64) + lane;
-        *rp = rew;
-        *dp = died ? 1 : 0;
+        const auto rr = buf_rsrc(p.reward ? p.reward + (int64_t)t * p.n : nullptr, (uint32_t)p.n * 4u);
+        const auto rd = buf_rsrc(p.done ? p.done + (int64_t)t * p.n : nullptr, (uint32_t)p.n);
+        __builtin_amdgcn_raw_buffer_store_b32(rew, rr, real ? (uint32_t)e * 4u : kOff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b8((char)(died ? 1 : 0), rd, real ? (uint32_t)e : kOff, 0, 0);
     };
     store_rd();
     if constexpr (KSTEPS == 1) {
@@ -773,24 +831,34 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         // the locked piece (R8: _set_piece(False), :303); a same-step reset:
         // the empty board.  The obs overlay of every non-spawning lane is then
         // painted (a death's terminal obs = L with its piece, :301).
+        // Only rows (board columns x) that one of the lane's 4 envs changed are
+        // written (buffer stores, see buf_rsrc).
         if (died && !reset_now) erase(L, lane, desc.x, desc.y, ax, ay, hmask);
+        if (died) bdirty = ~0u;
         KM[lane] = reset_now ? 0u : hmask;
+        BD[lane] = bdirty;
         __syncthreads();
         const uint4 km = *reinterpret_cast<const uint4 *>(&KM[lcc]);
+        const uint4 bd4 = *reinterpret_cast<const uint4 *>(&BD[lcc]);
+        const uint32_t bdl = (bd4.x | bd4.y | bd4.z | bd4.w) >> lrow;
         uint4 bw[NBQ];
 #pragma unroll
         for (int q = 0; q < NBQ; ++q)
             if (WT || 4 * q < W) bw[q] = *reinterpret_cast<const uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]);
-        uint32_t *bdst = p.board + e0;
+        // the board array as one resource: byte offsets < W * stride * 4 <= 2^31
+        const auto rb = buf_rsrc(p.board, (uint32_t)W * (uint32_t)sd * 4u);
+        const uint32_t boff = ((uint32_t)e0 * 4u + loff * 4u);
 #pragma unroll
         for (int q = 0; q < NBQ; ++q) {
-            if (WT || 4 * q < W) {  // rows >= W: padding rows of the allocation
+            if (WT || 4 * q < W) {
                 uint4 v = bw[q];
                 v.x &= km.x;
                 v.y &= km.y;
                 v.z &= km.z;
                 v.w &= km.w;
-                *reinterpret_cast<uint4 *>(bdst + (size_t)(4 * q) * sd + loff) = v;
+                // row 4q + lrow; padding rows (>= W) are never dirty
+                const bool dirty = (bdl >> (4 * q)) & 1u && 4 * q + lrow < W;
+                buf_store16(rb, dirty ? boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff, v);
             }
         }
         __syncthreads();  // the board reads above precede the overlay paint
@@ -832,17 +900,27 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         st[ST_STAT_EP_HOLES * sd] = holes;
         time = score = lines = holes = height = 0;
     }
+    // st_step stores only the counter rows that changed (sdirty, per env)
+    [[maybe_unused]] uint32_t sdirty = (1u << ST_STAT_TIME) | (1u << kPieceRow);
     ss(ST_STAT_TIME) = (uint32_t)time;
     ss(kPieceRow) = pw_out;
     if (locknow) {
-        ss(ST_STAT_SCORE) = (uint32_t)score;
-        ss(ST_STAT_LINES) = (uint32_t)lines;
-        ss(ST_STAT_HOLES) = (uint32_t)holes;
-        ss(ST_STAT_PIECE_HEIGHT) = (uint32_t)height;
-        ss(ST_STAT_DEATHS) = (uint32_t)deaths;
-        ss(ST_STAT_MT_INDEX) = (uint32_t)mtidx;
-        if (draw) atomicAdd(&ss(ST_STAT_COUNT0 + pick), 1u);  // shape_counts[name] += 1, :199 (ds_add, no return)
+        auto put = [&](int r, int32_t v) {
+            if constexpr (KSTEPS == 1) sdirty |= (uint32_t)(ss(r) != (uint32_t)v) << r;
+            ss(r) = (uint32_t)v;
+        };
+        put(ST_STAT_SCORE, score);
+        put(ST_STAT_LINES, lines);
+        put(ST_STAT_HOLES, holes);
+        put(ST_STAT_PIECE_HEIGHT, height);
+        put(ST_STAT_DEATHS, deaths);
+        put(ST_STAT_MT_INDEX, mtidx);
+        if (draw) {
+            atomicAdd(&ss(ST_STAT_COUNT0 + pick), 1u);  // shape_counts[name] += 1, :199 (ds_add, no return)
+            sdirty |= 1u << (ST_STAT_COUNT0 + pick);
+        }
     }
+    if constexpr (KSTEPS == 1) SD[lane] = sdirty;
 
     // ---- observation (tetris_env.py:301-302): board + current piece ----
     if (KSTEPS != 1 || spawn) paint(L, lane, odesc.x, odesc.y, oax, oay, hmask);
@@ -933,11 +1011,20 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         }
     }
     uint32_t *sdst = reinterpret_cast<uint32_t *>(p.stats) + e0;
+    uint32_t sdl = ~0u;  // rows to store: all (rollout) or those one of the lane's 4 envs changed
+    if constexpr (KSTEPS == 1) {
+        const uint4 sd4 = *reinterpret_cast<const uint4 *>(&SD[lcc]);
+        sdl = (sd4.x | sd4.y | sd4.z | sd4.w) >> lrow;
+    }
+    const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
+    const uint32_t soff = (uint32_t)e0 * 4u + loff * 4u;
+    (void)sdst;
 #pragma unroll
     for (int q = 0; q < kHotQ; ++q) {
-        if (4 * q + lrow < kHotRows)  // row 15 (ep_time) may have been stored per lane
-            *reinterpret_cast<uint4 *>(sdst + (size_t)(4 * q) * sd + loff) =
-                *reinterpret_cast<const uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]);
+        // row 15 (ep_time) is never staged: it is stored per lane on a reset
+        const bool st = 4 * q + lrow < kHotRows && ((sdl >> (4 * q)) & 1u);
+        buf_store16(rs, st ? soff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff,
+                    *reinterpret_cast<const uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]));
     }
     if constexpr (STAMP && KSTEPS == 1) {
         ST_STAMP(6);
