@@ -12,9 +12,9 @@ constexpr int kPad = 4;        // wall columns on each side of the LDS board
 constexpr int kMaxW = 32;
 constexpr int kMaxH = 28;
 constexpr int kMtN = 624;
-// diagnostic stamps per wave: 8 s_memtime phase stamps, s_memrealtime at
-// start and end, HW_ID, XCC_ID
-constexpr int kStampWords = 12;
+// diagnostic stamps per wave: 9 s_memtime phase stamps, s_memrealtime at
+// start and end, HW_ID, XCC_ID (16 words)
+constexpr int kStampWords = 16;
 constexpr int kPieceRow = ST_STAT_PIECE;     // rows 0..14 (counters + piece) move every step
 constexpr int kHotRows = ST_STAT_PIECE + 1;
 constexpr int kHotQ = (kHotRows * 16 + kWave - 1) / kWave;  // 16-B slots per lane

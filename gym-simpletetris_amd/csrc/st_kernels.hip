@@ -283,7 +283,7 @@ __device__ __forceinline__ void prefetch_words(const uint32_t *g, int32_t mtidx,
     if (want) {
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-            w[j] = __builtin_nontemporal_load(g + (mtidx + j < kMtN ? mtidx + j : kMtN - 1));
+            w[j] = g[mtidx + j < kMtN ? mtidx + j : kMtN - 1];  // cached (nt: packed rollout -12%)
     }
 }
 
@@ -553,7 +553,7 @@ __device__ __forceinline__ uint32_t pack_piece(int id, int rot, int ax, int ay, 
 // outputs at [t].  State is loaded once at the start and stored once at the end.
 template <int WT, int HT, bool F32, bool STAMP, int KSTEPS>
 __device__ __forceinline__ void run_steps(const KParams &p) {
-    [[maybe_unused]] uint64_t tstamp[8] = {};
+    [[maybe_unused]] uint64_t tstamp[9] = {};
     [[maybe_unused]] uint64_t rt0 = 0;
     if constexpr (STAMP) rt0 = __builtin_amdgcn_s_memrealtime();
     ST_STAMP(0);
@@ -865,6 +865,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         if (!spawn) paint(L, lane, desc.x, desc.y, ax, ay, hmask);
     }
 
+    ST_STAMP(8);  // (stamp 8: between the early stores and the draw)
     // ---- spawn (:299 _new_piece) or same-step reset (:306-315) ----
     int32_t cnt[7];
 #pragma unroll
@@ -1032,11 +1033,11 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         ST_STAMP(7);
         if (lane == 0) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) p.stamps[blockIdx.x * kStampWords + i] = tstamp[i];
-            p.stamps[blockIdx.x * kStampWords + 8] = rt0;
-            p.stamps[blockIdx.x * kStampWords + 9] = __builtin_amdgcn_s_memrealtime();
-            p.stamps[blockIdx.x * kStampWords + 10] = __builtin_amdgcn_s_getreg(0xF804);  // HW_ID
-            p.stamps[blockIdx.x * kStampWords + 11] = __builtin_amdgcn_s_getreg(0xF814);  // XCC_ID
+            for (int i = 0; i < 9; ++i) p.stamps[blockIdx.x * kStampWords + i] = tstamp[i];
+            p.stamps[blockIdx.x * kStampWords + 9] = rt0;
+            p.stamps[blockIdx.x * kStampWords + 10] = __builtin_amdgcn_s_memrealtime();
+            p.stamps[blockIdx.x * kStampWords + 11] = __builtin_amdgcn_s_getreg(0xF804);  // HW_ID
+            p.stamps[blockIdx.x * kStampWords + 12] = __builtin_amdgcn_s_getreg(0xF814);  // XCC_ID
         }
     }
 }
