@@ -12,7 +12,7 @@ constexpr int kPad = 4;        // wall columns on each side of the LDS board
 constexpr int kMaxW = 32;
 constexpr int kMaxH = 28;
 constexpr int kMtN = 624;
-// diagnostic stamps per wave: 9 s_memtime phase stamps, s_memrealtime at
+// diagnostic stamps per wave: 10 s_memtime phase stamps, s_memrealtime at
 // start and end, HW_ID, XCC_ID (16 words)
 constexpr int kStampWords = 16;
 constexpr int kPieceRow = ST_STAT_PIECE;     // rows 0..14 (counters + piece) move every step

@@ -308,10 +308,30 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], int32_t 
     // registers would wait vmcnt(0) -- draining the caller's early stores.
     asm volatile("" ::"v"(pre[0]), "v"(pre[1]), "v"(pre[2]), "v"(pre[3]), "v"(pre[4]), "v"(pre[5]),
                  "v"(pre[6]), "v"(pre[7]));
-    uint32_t w[8];
+    // Fast path, branch-free: temper all 8 prefetched words (independent
+    // chains) and take each lane's first accepted one.  Lanes it does not
+    // settle (8 rejections, p <= 2^-8, or the state's end: a twist) continue
+    // in the loop below past the 8 words.
+    if (have_pre && pending && mtidx < kMtN) {
+        int first = 8;
+        uint32_t rr = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) w[j] = pre[j];
-    bool have = have_pre && pending && mtidx < kMtN;  // first round: words prefetched by the caller
+        for (int j = 7; j >= 0; --j) {
+            const uint32_t y = mt_temper(pre[j]) >> (32 - k);
+            const bool acc = y < n && mtidx + j < kMtN;
+            first = acc ? j : first;
+            rr = acc ? y : rr;
+        }
+        if (first < 8) {
+            pending = false;
+            r = rr;
+            mtidx += first + 1;
+        } else {
+            mtidx = mtidx + 8 < kMtN ? mtidx + 8 : kMtN;
+        }
+    }
+    uint32_t w[8];
+    bool have = false;
     while (__ballot(pending)) {
         if (!twist && pending && mtidx >= kMtN) mtidx = 0;  // ablation: skip the twist
         uint64_t tw = __ballot(pending && mtidx >= kMtN);
@@ -553,7 +573,7 @@ __device__ __forceinline__ uint32_t pack_piece(int id, int rot, int ax, int ay, 
 // outputs at [t].  State is loaded once at the start and stored once at the end.
 template <int WT, int HT, bool F32, bool STAMP, int KSTEPS>
 __device__ __forceinline__ void run_steps(const KParams &p) {
-    [[maybe_unused]] uint64_t tstamp[9] = {};
+    [[maybe_unused]] uint64_t tstamp[10] = {};
     [[maybe_unused]] uint64_t rt0 = 0;
     if constexpr (STAMP) rt0 = __builtin_amdgcn_s_memrealtime();
     ST_STAMP(0);
@@ -871,6 +891,10 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
 #pragma unroll
     for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)ss(ST_STAT_COUNT0 + i);  // used by drawing lanes only
     int pick = 0;
+    if constexpr (STAMP) {  // diagnostic split of the draw: MT-word wait | compute
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ST_STAMP(9);
+    }
     if (!(p.ablate & 2u)) {
         if constexpr (!kRing) {
             pick = draw_shape(draw, cnt, mtidx, p.mt + e0 * kMtN, S, lane, !(p.ablate & 4u), pre,
@@ -1033,11 +1057,11 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         ST_STAMP(7);
         if (lane == 0) {
 #pragma unroll
-            for (int i = 0; i < 9; ++i) p.stamps[blockIdx.x * kStampWords + i] = tstamp[i];
-            p.stamps[blockIdx.x * kStampWords + 9] = rt0;
-            p.stamps[blockIdx.x * kStampWords + 10] = __builtin_amdgcn_s_memrealtime();
-            p.stamps[blockIdx.x * kStampWords + 11] = __builtin_amdgcn_s_getreg(0xF804);  // HW_ID
-            p.stamps[blockIdx.x * kStampWords + 12] = __builtin_amdgcn_s_getreg(0xF814);  // XCC_ID
+            for (int i = 0; i < 10; ++i) p.stamps[blockIdx.x * kStampWords + i] = tstamp[i];
+            p.stamps[blockIdx.x * kStampWords + 10] = rt0;
+            p.stamps[blockIdx.x * kStampWords + 11] = __builtin_amdgcn_s_memrealtime();
+            p.stamps[blockIdx.x * kStampWords + 12] = __builtin_amdgcn_s_getreg(0xF804);  // HW_ID
+            p.stamps[blockIdx.x * kStampWords + 13] = __builtin_amdgcn_s_getreg(0xF814);  // XCC_ID
         }
     }
 }

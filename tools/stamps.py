@@ -20,16 +20,16 @@ nw = b.stride // 64
 W = 16  # kStampWords
 buf = np.zeros(nw * W, np.uint64)
 rts = []
-names = ["loads", "action+drop", "lock path", "early stores", "draw", "obs (+f32) issue", "state stores issue", "store drain"]
+names = ["loads", "action+drop", "lock path", "early stores", "store+MT wait", "draw", "obs (+f32) issue", "state stores issue", "store drain"]
 acc = []
 for t in range(300):
     b.step(b.gen_actions(t, 0x5EED), obs="f32" if f32 else "packed")
     if t >= 100:
         b._L.st_debug_stamps(b._ctx, ctypes.c_void_p(buf.ctypes.data), buf.size)
         full = buf.reshape(nw, W).astype(np.int64)
-        st = full[:, [0, 1, 2, 3, 8, 4, 5, 6, 7]]  # stamp 8 sits between 3 and 4
+        st = full[:, [0, 1, 2, 3, 8, 9, 4, 5, 6, 7]]  # stamps 8, 9 sit between 3 and 4
         acc.append(np.diff(st, axis=1))
-        rts.append(full[:, 9:13].copy())
+        rts.append(full[:, 10:14].copy())
 a = np.concatenate(acc)
 tot = (a.sum(1))
 print(f"f32={f32} waves={nw} steps=200  total cycles median {np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} max {tot.max()}")
