@@ -128,7 +128,8 @@ int st_create(st_ctx **out, const st_config *cfg, int device, int64_t n_envs) {
     if (e == hipSuccess) e = hipMalloc(&c->board, sd * wpad * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&c->stats, sd * ST_NSTAT * sizeof(int32_t));
     if (e == hipSuccess) c->piece = reinterpret_cast<uint32_t *>(c->stats) + ST_STAT_PIECE * sd;
-    if (e == hipSuccess) e = hipMalloc(&c->mt, sd * st::kMtN * sizeof(uint32_t));
+    // + 8 words: the step kernel's 8-word MT prefetch may read past the last env's state
+    if (e == hipSuccess) e = hipMalloc(&c->mt, (sd * st::kMtN + 8) * sizeof(uint32_t));
     if (e == hipSuccess && getenv("ST_STAMPS"))
         e = hipMalloc(&c->stamps, (sd / st::kWave) * st::kStampWords * sizeof(uint64_t));
     if (e != hipSuccess) {

@@ -105,7 +105,14 @@ __constant__ uint32_t c_tab_g[28] = ST_TAB28(kTab.g);
 // tetris_env.py:32-33; _set_piece clips them, :326).
 __device__ __forceinline__ int pc_dx(uint32_t g, int j) { return (int)((g >> (6 * j)) & 7u) - 3; }
 __device__ __forceinline__ int pc_bot(uint32_t g, int j) { return (int)((g >> (6 * j + 3)) & 7u) - 3; }
+// S32: board height <= 25 (compile time), so a cell's bit (row + 3 <= 30)
+// fits a 32-bit shift.  (The 64-bit form's don't-care high half can land in
+// a register still waiting on a load -- measured: the lock path's paint
+// waited for the MT prefetch -- so the 32-bit form is used wherever it is
+// exact.)
+template <bool S32 = false>
 __device__ __forceinline__ uint32_t pc_bits(uint32_t m, int j, int y) {
+    if constexpr (S32) return (((m >> (8 * j)) & 0xFFu) << y) >> 3;
     return (uint32_t)((uint64_t)((m >> (8 * j)) & 0xFFu) << y >> 3);
 }
 
@@ -144,10 +151,11 @@ __device__ __forceinline__ void read_cols(const uint32_t *L, int lane, uint32_t 
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = L[(x + pc_dx(g, j) + kPad) * kWave + lane];
 }
+template <bool S32 = false>
 __device__ __forceinline__ bool collides_v(uint32_t m, int y, const uint32_t (&v)[4]) {
     uint32_t hit = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) hit |= pc_bits(m, j, y) & v[j];
+    for (int j = 0; j < 4; ++j) hit |= pc_bits<S32>(m, j, y) & v[j];
     return hit != 0;
 }
 __device__ __forceinline__ int drop_v(uint32_t g, int y, const uint32_t (&v)[4]) {
@@ -164,19 +172,21 @@ __device__ __forceinline__ int drop_v(uint32_t g, int y, const uint32_t (&v)[4])
 
 // _set_piece(True) (tetris_env.py:323-327): cells inside the board only,
 // as no-return LDS atomics.
+template <bool S32 = false>
 __device__ __forceinline__ void paint(uint32_t *L, int lane, uint32_t m, uint32_t g, int x, int y,
                                       uint32_t hmask) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-        atomicOr(&L[(x + pc_dx(g, j) + kPad) * kWave + lane], pc_bits(m, j, y) & hmask);  // ds_or_b32
+        atomicOr(&L[(x + pc_dx(g, j) + kPad) * kWave + lane], pc_bits<S32>(m, j, y) & hmask);  // ds_or_b32
 }
 
 // _set_piece(False): erase the cells.
+template <bool S32 = false>
 __device__ __forceinline__ void erase(uint32_t *L, int lane, uint32_t m, uint32_t g, int x, int y,
                                       uint32_t hmask) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-        atomicAnd(&L[(x + pc_dx(g, j) + kPad) * kWave + lane], ~(pc_bits(m, j, y) & hmask));
+        atomicAnd(&L[(x + pc_dx(g, j) + kPad) * kWave + lane], ~(pc_bits<S32>(m, j, y) & hmask));
 }
 
 // _clear_lines row compaction (tetris_env.py:205-216) on one column word:
@@ -209,7 +219,7 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
 // all 64 lanes, wave-uniformly).  The serial recurrence splits into four
 // chunks whose elements only read OLD words or words of earlier chunks:
 // [0,227) old | [227,454) uses [0,227) | [454,623) uses [227,396) | 623.
-__device__ void coop_twist(uint32_t *g, uint32_t *S, int lane) {
+__device__ __noinline__ void coop_twist(uint32_t *g, uint32_t *S, int lane) {
     {
         uint32_t t[10];  // 624 = 9 * 64 + 48: issue all ten loads before any wait
 #pragma unroll
@@ -277,13 +287,14 @@ __device__ void coop_twist(uint32_t *g, uint32_t *S, int lane) {
 // the lock-path work).
 __device__ __forceinline__ void prefetch_words(const uint32_t *g, int32_t mtidx, bool want,
                                                uint32_t (&w)[8]) {
-    // one exec region; indices clamped (words past the state are never consumed)
+    // one exec region; words past index 623 are read but never consumed
 #pragma unroll
     for (int j = 0; j < 8; ++j) w[j] = 0u;
     if (want) {
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-            w[j] = g[mtidx + j < kMtN ? mtidx + j : kMtN - 1];  // cached (nt: packed rollout -12%)
+            w[j] = g[mtidx + j];  // cached (nt: packed rollout -12%); reads past the env's
+                                  // state land in the next env's or the allocation's 8-word pad
     }
 }
 
@@ -574,6 +585,7 @@ __device__ __forceinline__ uint32_t pack_piece(int id, int rot, int ax, int ay, 
 template <int WT, int HT, bool F32, bool STAMP, int KSTEPS>
 __device__ __forceinline__ void run_steps(const KParams &p) {
     [[maybe_unused]] uint64_t tstamp[10] = {};
+    constexpr bool S32 = HT != 0 && HT <= 25;  // see pc_bits
     [[maybe_unused]] uint64_t rt0 = 0;
     if constexpr (STAMP) rt0 = __builtin_amdgcn_s_memrealtime();
     ST_STAMP(0);
@@ -712,7 +724,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     read_cols(L, lane, cdesc.y, cx, cand);
     // branch-free: select the accepted position's descriptor and columns, then
     // one drop test (both arms would otherwise run in a divergent wave)
-    const bool ok = tries && !collides_v(cdesc.x, ay, cand);
+    const bool ok = tries && !collides_v<S32>(cdesc.x, ay, cand);
     ax = ok ? cx : ax;
     rot = ok ? cr : rot;
     desc.x = ok ? cdesc.x : desc.x;
@@ -759,7 +771,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         holes = (int32_t)ss(ST_STAT_HOLES);
         height = (int32_t)ss(ST_STAT_PIECE_HEIGHT);
         deaths = (int32_t)ss(ST_STAT_DEATHS);
-        paint(L, lane, desc.x, desc.y, ax, ay, hmask);
+        paint<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
         // Column words carry the floor bits, so the topmost cell of column v
         // is ctz(v) (H when empty) and its holes are H - ctz(v) - popc(v & hmask):
         // summed, holes = W*H - sum ctz(v) - (sum popc(v) - W*(32-H)).
@@ -853,7 +865,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         // painted (a death's terminal obs = L with its piece, :301).
         // Only rows (board columns x) that one of the lane's 4 envs changed are
         // written (buffer stores, see buf_rsrc).
-        if (died && !reset_now) erase(L, lane, desc.x, desc.y, ax, ay, hmask);
+        if (died && !reset_now) erase<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
         if (died) bdirty = ~0u;
         KM[lane] = reset_now ? 0u : hmask;
         BD[lane] = bdirty;
@@ -882,7 +894,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
             }
         }
         __syncthreads();  // the board reads above precede the overlay paint
-        if (!spawn) paint(L, lane, desc.x, desc.y, ax, ay, hmask);
+        if (!spawn) paint<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
     }
 
     ST_STAMP(8);  // (stamp 8: between the early stores and the draw)
@@ -948,7 +960,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     if constexpr (KSTEPS == 1) SD[lane] = sdirty;
 
     // ---- observation (tetris_env.py:301-302): board + current piece ----
-    if (KSTEPS != 1 || spawn) paint(L, lane, odesc.x, odesc.y, oax, oay, hmask);
+    if (KSTEPS != 1 || spawn) paint<S32>(L, lane, odesc.x, odesc.y, oax, oay, hmask);
     __syncthreads();
     const bool wide_obs = (p.n & 3) == 0 && e0 + kWave <= p.n &&
                           (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0;
@@ -1015,7 +1027,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         // lane: non-locking lanes and spawns (overlay cells were empty), and a
         // death without auto-reset (R8: _set_piece(False), tetris_env.py:303).
         __syncthreads();
-        erase(L, lane, odesc.x, odesc.y, oax, oay, hmask);
+        erase<S32>(L, lane, odesc.x, odesc.y, oax, oay, hmask);
         if (reset_now)
             for (int x = 0; x < W; ++x) lcol(L, x, lane) = floorb;
     }
