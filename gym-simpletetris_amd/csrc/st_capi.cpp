@@ -278,6 +278,79 @@ int st_state(st_ctx *c, st_state_views *out) {
     return ST_OK;
 }
 
+namespace {
+struct SnapHeader {  // st_save / st_load, 64 bytes
+    char magic[8];
+    uint32_t abi;
+    int32_t width, height, nstat;
+    int64_t n;
+    uint8_t pad[32];
+};
+static_assert(sizeof(SnapHeader) == 64, "snapshot header");
+const char kSnapMagic[8] = {'S', 'T', 'S', 'N', 'A', 'P', 0, 1};
+
+int64_t snap_bytes(const st_ctx *c) {
+    return (int64_t)sizeof(SnapHeader) +
+           c->n * 4 * ((int64_t)c->cfg.width + ST_NSTAT + st::kMtN);
+}
+}  // namespace
+
+int64_t st_state_bytes(const st_ctx *c) { return c ? snap_bytes(c) : -1; }
+
+int st_save(st_ctx *c, void *host_out, int64_t bytes) {
+    if (!c || !host_out) return fail(ST_EINVAL, "st_save: null argument");
+    if (bytes != snap_bytes(c))
+        return fail(ST_EINVAL, "st_save: buffer is %lld bytes, a snapshot is %lld", (long long)bytes,
+                    (long long)snap_bytes(c));
+    DeviceGuard g(c->device);
+    SnapHeader h{};
+    memcpy(h.magic, kSnapMagic, sizeof(h.magic));
+    h.abi = ST_ABI_VERSION;
+    h.width = c->cfg.width;
+    h.height = c->cfg.height;
+    h.nstat = ST_NSTAT;
+    h.n = c->n;
+    char *o = static_cast<char *>(host_out);
+    memcpy(o, &h, sizeof(h));
+    o += sizeof(h);
+    const size_t row = (size_t)c->n * 4, pitch = (size_t)c->stride * 4;
+    ST_HIP(hipDeviceSynchronize());
+    ST_HIP(hipMemcpy2D(o, row, c->board, pitch, row, c->cfg.width, hipMemcpyDeviceToHost));
+    o += row * c->cfg.width;
+    ST_HIP(hipMemcpy2D(o, row, c->stats, pitch, row, ST_NSTAT, hipMemcpyDeviceToHost));
+    o += row * ST_NSTAT;
+    ST_HIP(hipMemcpy(o, c->mt, row * st::kMtN, hipMemcpyDeviceToHost));
+    return ST_OK;
+}
+
+int st_load(st_ctx *c, const void *host_in, int64_t bytes) {
+    if (!c || !host_in) return fail(ST_EINVAL, "st_load: null argument");
+    if (bytes != snap_bytes(c))
+        return fail(ST_EINVAL, "st_load: %lld bytes, this context's snapshot is %lld", (long long)bytes,
+                    (long long)snap_bytes(c));
+    SnapHeader h;
+    memcpy(&h, host_in, sizeof(h));
+    if (memcmp(h.magic, kSnapMagic, sizeof(h.magic)) != 0) return fail(ST_EINVAL, "st_load: not a snapshot");
+    if (h.abi != ST_ABI_VERSION || h.nstat != ST_NSTAT)
+        return fail(ST_EINVAL, "st_load: snapshot of ABI %u (%d counter rows), this is %d (%d)", h.abi,
+                    h.nstat, ST_ABI_VERSION, ST_NSTAT);
+    if (h.width != c->cfg.width || h.height != c->cfg.height || h.n != c->n)
+        return fail(ST_EINVAL, "st_load: snapshot of %lld %dx%d envs, context has %lld %dx%d",
+                    (long long)h.n, h.width, h.height, (long long)c->n, c->cfg.width, c->cfg.height);
+    DeviceGuard g(c->device);
+    const char *in = static_cast<const char *>(host_in) + sizeof(h);
+    const size_t row = (size_t)c->n * 4, pitch = (size_t)c->stride * 4;
+    ST_HIP(hipDeviceSynchronize());
+    ST_HIP(hipMemcpy2D(c->board, pitch, in, row, row, c->cfg.width, hipMemcpyHostToDevice));
+    in += row * c->cfg.width;
+    ST_HIP(hipMemcpy2D(c->stats, pitch, in, row, row, ST_NSTAT, hipMemcpyHostToDevice));
+    in += row * ST_NSTAT;
+    ST_HIP(hipMemcpy(c->mt, in, row * st::kMtN, hipMemcpyHostToDevice));
+    ST_HIP(hipDeviceSynchronize());
+    c->seeded = c->reset_once = true;
+    return ST_OK;
+}
+
 int st_debug_stamps(st_ctx *c, uint64_t *host_out, int64_t max_words) {
     if (!c || !host_out) return fail(ST_EINVAL, "st_debug_stamps: null argument");
     if (!c->stamps) return fail(ST_ESTATE, "context was not created with ST_STAMPS set");

@@ -204,9 +204,11 @@ __device__ __forceinline__ uint32_t compact(uint32_t v, uint32_t full) {
 // ---------------------------------------------------------------- MT19937
 // CPython Modules/_randommodule.c genrand_uint32 / init_by_array.
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+    // y ^ (t & B) as one v_bitop3 (truth table 0x78 = a ^ (b & c) with the
+    // a=0xF0 / b=0xCC / c=0xAA convention)
     y ^= (y >> 11);
-    y ^= (y << 7) & 0x9d2c5680u;
-    y ^= (y << 15) & 0xefc60000u;
+    y = __builtin_amdgcn_bitop3_b32(y, y << 7, 0x9d2c5680u, 0x78);
+    y = __builtin_amdgcn_bitop3_b32(y, y << 15, 0xefc60000u, 0x78);
     y ^= (y >> 18);
     return y;
 }

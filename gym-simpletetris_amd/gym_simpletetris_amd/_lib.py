@@ -36,8 +36,8 @@ NSTAT = 19
 MT_N = 624
 
 EXPORTS = ("st_create", "st_destroy", "st_seed", "st_reset", "st_step", "st_step_f32", "st_rollout",
-           "st_obs_to_f32", "st_render", "st_grayscale", "st_state", "st_copy", "st_gen_actions", "st_debug_stamps",
-           "st_last_error", "st_abi_version")
+           "st_obs_to_f32", "st_render", "st_grayscale", "st_state", "st_copy", "st_state_bytes", "st_save",
+           "st_load", "st_gen_actions", "st_debug_stamps", "st_last_error", "st_abi_version")
 
 
 class StError(RuntimeError):
@@ -88,12 +88,18 @@ def load(path: str = LIB_PATH):
         "st_grayscale": ([vp, vp, i32, i32, i32, vp, vp], ctypes.c_int),
         "st_state": ([vp, ctypes.POINTER(StateViews)], ctypes.c_int),
         "st_copy": ([vp, vp, i64, vp], ctypes.c_int),
+        "st_state_bytes": ([vp], i64),
+        "st_save": ([vp, vp, i64], ctypes.c_int),
+        "st_load": ([vp, vp, i64], ctypes.c_int),
         "st_gen_actions": ([vp, i64, i64, u64, i64, vp], ctypes.c_int),
         "st_debug_stamps": ([vp, vp, i64], ctypes.c_int),
         "st_last_error": ([], ctypes.c_char_p),
         "st_abi_version": ([], ctypes.c_int),
     }
-    for name, (args, res) in sig.items():
+    ab_override = "ST_LIB" in os.environ  # diagnostic A/B of older builds: tolerate
+    for name, (args, res) in sig.items():  # entry points they predate
+        if ab_override and not hasattr(L, name):
+            continue
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res

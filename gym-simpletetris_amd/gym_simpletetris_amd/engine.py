@@ -8,6 +8,7 @@ the output buffers (torch tensors on the device) and the stream plumbing.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional, Sequence
 
 import numpy as np
@@ -258,6 +259,29 @@ class TetrisBatch:
                 C.check(self._L.st_copy(ctypes.c_void_p(self._view_ptr(f)), _ptr(t),
                                         t.numel() * 4, self._stream()))
             torch.cuda.synchronize(self.device)
+
+    def save(self, path: Optional[str] = None) -> bytes:
+        """Snapshot of every env's state (st_save: board, piece, counters,
+        shape counts, MT19937 state); written to `path` if given."""
+        nbytes = int(self._L.st_state_bytes(self._ctx))
+        buf = ctypes.create_string_buffer(nbytes)
+        with torch.cuda.device(self.device):
+            C.check(self._L.st_save(self._ctx, ctypes.cast(buf, ctypes.c_void_p), nbytes))
+        data = buf.raw
+        if path is not None:
+            with open(path, "wb") as f:
+                f.write(data)
+        return data
+
+    def load(self, snapshot) -> None:
+        """Restore a snapshot from save() (bytes or a file path) into this
+        batch (same width, height and env count)."""
+        if isinstance(snapshot, (str, os.PathLike)):
+            with open(snapshot, "rb") as f:
+                snapshot = f.read()
+        data = bytes(snapshot)
+        with torch.cuda.device(self.device):
+            C.check(self._L.st_load(self._ctx, data, len(data)))
 
     def render_packed(self, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """TetrisEngine.render() (tetris_env.py:317-321): board + current piece,

@@ -178,8 +178,23 @@ int st_grayscale(st_ctx *ctx, const uint32_t *d_obs, int32_t size, int32_t chann
 int st_state(st_ctx *ctx, st_state_views *out);
 
 /* hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, stream) -- moves state
- * between the views above and caller buffers (save/load, crafted states). */
+ * between the views above and caller buffers (crafted states). */
 int st_copy(void *dst, const void *src, int64_t bytes, st_stream stream);
+
+/* State snapshot: the engine attributes of every env (board, piece, counters,
+ * shape counts: TetrisEngine.__init__ / _new_piece, tetris_env.py:138-199)
+ * and its MT19937 state (CPython random.getstate(), :187).
+ * st_state_bytes: the size of one snapshot of this context.
+ * st_save: writes it to host memory (a 64-byte header -- magic "STSNAP\0\1",
+ *   ABI version, width, height, ST_NSTAT, n_envs -- then board uint32
+ *   [width][n_envs], stats int32 [ST_NSTAT][n_envs], mt uint32 [n_envs][624]).
+ * st_load: restores one into a context with the same width, height and
+ *   n_envs (scoring flags and lock delay are configuration, not state, and
+ *   may differ).  A loaded context needs no st_seed / st_reset.
+ * Both synchronous; ST_EINVAL on a size or header mismatch. */
+int64_t st_state_bytes(const st_ctx *ctx);
+int st_save(st_ctx *ctx, void *host_out, int64_t bytes);
+int st_load(st_ctx *ctx, const void *host_in, int64_t bytes);
 
 /* Synthetic action source used by the benchmark and the parity tests:
  * d_out[e] = splitmix64(seed ^ ((t << 32) ^ (global_offset + e))) % 7. */
@@ -188,8 +203,9 @@ int st_gen_actions(uint8_t *d_out, int64_t n, int64_t t, uint64_t seed,
 
 /* Diagnostics: when the environment variable ST_STAMPS is set at st_create,
  * st_step runs an instrumented build of the step kernel that records
- * s_memtime at 8 phase boundaries per wave; this copies the last step's
- * stamps ([n_waves][8] uint64) to host memory.  Timing study only. */
+ * s_memtime at its phase boundaries per wave; this copies the last step's
+ * stamps ([n_waves][16] uint64: 10 phase stamps, s_memrealtime at start and
+ * end, HW_ID, XCC_ID) to host memory.  Timing study only. */
 int st_debug_stamps(st_ctx *ctx, uint64_t *host_out, int64_t max_words);
 
 /* Message for the last failed call on this thread ("" if none). */
