@@ -22,6 +22,7 @@ struct st_ctx {
     uint32_t *piece;
     int32_t *stats;
     uint32_t *mt;
+    uint32_t *mt_alloc;  // mt - kMtPadFront
 };
 
 namespace {
@@ -81,10 +82,10 @@ st::KParams params(const st_ctx *c) {
 void free_state(st_ctx *c) {
     if (c->board) (void)hipFree(c->board);
     if (c->stats) (void)hipFree(c->stats);
-    if (c->mt) (void)hipFree(c->mt);
+    if (c->mt_alloc) (void)hipFree(c->mt_alloc);
     if (c->stamps) (void)hipFree(c->stamps);
     c->stamps = nullptr;
-    c->board = c->piece = c->mt = nullptr;
+    c->board = c->piece = c->mt = c->mt_alloc = nullptr;
     c->stats = nullptr;
 }
 
@@ -128,8 +129,12 @@ int st_create(st_ctx **out, const st_config *cfg, int device, int64_t n_envs) {
     if (e == hipSuccess) e = hipMalloc(&c->board, sd * wpad * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&c->stats, sd * ST_NSTAT * sizeof(int32_t));
     if (e == hipSuccess) c->piece = reinterpret_cast<uint32_t *>(c->stats) + ST_STAT_PIECE * sd;
-    // + 8 words: the step kernel's 8-word MT prefetch may read past the last env's state
-    if (e == hipSuccess) e = hipMalloc(&c->mt, (sd * st::kMtN + 8) * sizeof(uint32_t));
+    // MT states with pads: a draw's window reads words idx-227.. and idx+397..
+    // of its own state unconditionally, which for the first / last env fall
+    // outside the states (values never used)
+    if (e == hipSuccess)
+        e = hipMalloc(&c->mt_alloc, (st::kMtPadFront + sd * st::kMtN + st::kMtPadBack) * sizeof(uint32_t));
+    if (e == hipSuccess) c->mt = c->mt_alloc + st::kMtPadFront;
     if (e == hipSuccess && getenv("ST_STAMPS"))
         e = hipMalloc(&c->stamps, (sd / st::kWave) * st::kStampWords * sizeof(uint64_t));
     if (e != hipSuccess) {
@@ -227,6 +232,13 @@ int st_rollout(st_ctx *c, int32_t k, const uint8_t *d_actions, uint32_t *d_obs, 
     return ST_OK;
 }
 
+int st_mt_sync(st_ctx *c, st_stream stream) {
+    if (!c) return fail(ST_EINVAL, "st_mt_sync: null context");
+    DeviceGuard g(c->device);
+    ST_HIP(st::launch_mt_sync(params(c), (hipStream_t)stream));
+    return ST_OK;
+}
+
 int st_obs_to_f32(st_ctx *c, const uint32_t *d_obs, float *d_out, st_stream stream) {
     if (!c || !d_obs || !d_out) return fail(ST_EINVAL, "st_obs_to_f32: null argument");
     DeviceGuard g(c->device);
@@ -314,6 +326,8 @@ int st_save(st_ctx *c, void *host_out, int64_t bytes) {
     memcpy(o, &h, sizeof(h));
     o += sizeof(h);
     const size_t row = (size_t)c->n * 4, pitch = (size_t)c->stride * 4;
+    ST_HIP(hipDeviceSynchronize());
+    ST_HIP(st::launch_mt_sync(params(c), nullptr));  // CPython's MT state in the snapshot
     ST_HIP(hipDeviceSynchronize());
     ST_HIP(hipMemcpy2D(o, row, c->board, pitch, row, c->cfg.width, hipMemcpyDeviceToHost));
     o += row * c->cfg.width;

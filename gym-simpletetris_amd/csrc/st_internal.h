@@ -12,6 +12,10 @@ constexpr int kPad = 4;        // wall columns on each side of the LDS board
 constexpr int kMaxW = 32;
 constexpr int kMaxH = 28;
 constexpr int kMtN = 624;
+// MT allocation pads (words): a draw window reads idx-227..idx-220 and
+// idx+397..idx+407 of its env's state for any idx in [0, 624)
+constexpr int64_t kMtPadFront = 256;
+constexpr int64_t kMtPadBack = 512;
 // diagnostic stamps per wave: 10 s_memtime phase stamps, s_memrealtime at
 // start and end, HW_ID, XCC_ID (16 words)
 constexpr int kStampWords = 16;
@@ -53,6 +57,7 @@ hipError_t launch_step(const KParams &p, hipStream_t s);
 hipError_t launch_rollout(const KParams &p, hipStream_t s);
 hipError_t launch_obs_f32(const KParams &p, const uint32_t *obs, float *out, hipStream_t s);
 hipError_t launch_render(const KParams &p, hipStream_t s);
+hipError_t launch_mt_sync(const KParams &p, hipStream_t s);
 hipError_t launch_grayscale(const KParams &p, const uint32_t *obs, int size, int channels,
                             int as_u8, void *out, hipStream_t s);
 hipError_t launch_gen_actions(uint8_t *out, int64_t n, int64_t t, uint64_t seed, int64_t off,

@@ -18,11 +18,6 @@
 // bounds checks and hard_drop is a count-trailing-zeros per piece column.
 #include "st_internal.h"
 
-// st_rollout draws from a per-lane LDS ring of MT words (1) or, like st_step,
-// from words prefetched when the lane locks (0).  Diagnostic A/B switch.
-#ifndef ST_RING
-#define ST_RING 1
-#endif
 
 namespace st {
 namespace {
@@ -201,6 +196,17 @@ __device__ __forceinline__ uint32_t compact(uint32_t v, uint32_t full) {
     return v;
 }
 
+// Every kernel below that exchanges data between lanes through LDS runs one
+// wave per workgroup.  LDS operations of a wavefront execute in order, so a
+// read issued after another lane's write returns that write's data: the
+// exchange needs only compiler ordering, not __syncthreads' full
+// s_waitcnt lgkmcnt(0) (which would stall the wave for each LDS round trip).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ---------------------------------------------------------------- MT19937
 // CPython Modules/_randommodule.c genrand_uint32 / init_by_array.
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
@@ -217,11 +223,215 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
     return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
 }
 
-// Wave-cooperative twist of ONE env's 624-word state `g` (must be called by
-// all 64 lanes, wave-uniformly).  The serial recurrence splits into four
-// chunks whose elements only read OLD words or words of earlier chunks:
-// [0,227) old | [227,454) uses [0,227) | [454,623) uses [227,396) | 623.
-__device__ __noinline__ void coop_twist(uint32_t *g, uint32_t *S, int lane) {
+// ---- Incremental twist -------------------------------------------------------
+// CPython refills its 624 words all at once when the index reaches 624:
+//   mt[k] = X_k ^ mix(mt[k], mt[k+1]),  X_k = mt[k+397] (k < 227) | mt[k-227] (k >= 227),
+//   and mt[623] = mt[396] ^ mix(mt[623], mt[0]),
+// in place, in index order.  Evaluated in the same order one word at a time,
+// every operand is old exactly where CPython's is old (mt[k], mt[k+1],
+// mt[k+397]) and new where CPython's is new (mt[k-227], mt[396], mt[0]), so a
+// generation can be materialized lazily, as draws reach it: no wave ever runs
+// the 624-word twist (which made a twisting wave 2x slower than the others and
+// set the step's length whenever one occurred).
+//
+// State encoding (stats row ST_STAT_MT_INDEX): idx | (M << 16).
+//   M = 0      : CPython's state -- every word of the current generation, idx =
+//                CPython's index (624: the next draw starts a generation).
+//   M = m + 1  : a generation in progress: words [0, m) new, [m, 624) of the
+//                previous generation, idx <= m.
+// st_mt_sync (k_mt_sync) completes pending generations before the host reads
+// the state; every writer of state from the host writes M = 0.
+__device__ __forceinline__ void mt_unpack(uint32_t r, int &idx, int &m) {
+    idx = (int)(r & 0xFFFFu);
+    m = (r >> 16) ? (int)(r >> 16) - 1 : kMtN;
+}
+__device__ __forceinline__ uint32_t mt_pack(int idx, int m) {
+    return (uint32_t)idx | (m < kMtN ? (uint32_t)(m + 1) << 16 : 0u);
+}
+// A complete generation that has been used up starts the next one (lazily).
+__device__ __forceinline__ void mt_begin(int &idx, int &m) {
+    if (idx >= kMtN && m >= kMtN) {
+        idx = 0;
+        m = 0;
+    }
+}
+
+// The 8 words a draw reads at index idx (idx < 624), and the operands that
+// materialize those not yet of the current generation.  a[0..8]: words
+// idx..idx+8 (a[j + 1] = mt[k+1]); bhi / blo: words idx+397.. / idx-227.. (X_k
+// for k < 227 / k >= 227, also mt[396] for k = 623); w0 = mt[0].  Buffer
+// loads through the wave's MT resource (mt_res): lanes or operands not wanted
+// get an out-of-range offset and read 0, so every load is issued on one path
+// (no branch, no merge of loaded and zero registers that would make the
+// compiler wait for the loads right here).  Reads past an env's state land in
+// a neighbour's state or the allocation's pads (values never used).
+struct MtWin {
+    uint32_t a[12], bhi[8], blo[8], w0;
+};
+struct MtRes {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t lane_off;  // byte offset of this lane's word 0
+};
+__device__ __forceinline__ MtRes mt_res(uint32_t *mt_wave, int lane) {
+    MtRes m;
+    m.r = buf_rsrc(mt_wave - kMtPadFront, (uint32_t)((kWave * kMtN + kMtPadFront + kMtPadBack) * 4));
+    m.lane_off = (uint32_t)(lane * kMtN + kMtPadFront) * 4u;
+    return m;
+}
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void mt_win_load(const MtRes &rs, int idx, int m, bool want, MtWin &w) {
+    const uint32_t base = rs.lane_off + 4u * (uint32_t)idx;
+#ifdef ST_AB_NOHI
+    const bool hi = false;
+#else
+    const bool hi = want && idx + 8 > m;  // the window reaches words of the previous generation
+#endif
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {  // cached loads (nt: packed rollout -12%)
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs.r, want ? base + 16u * q : kOff, 0, 0);
+        w.a[4 * q] = v.x, w.a[4 * q + 1] = v.y, w.a[4 * q + 2] = v.z, w.a[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const u32x4 h = __builtin_amdgcn_raw_buffer_load_b128(rs.r, hi ? base + 4u * 397u + 16u * q : kOff, 0, 0);
+        const u32x4 l = __builtin_amdgcn_raw_buffer_load_b128(rs.r, hi ? base - 4u * 227u + 16u * q : kOff, 0, 0);
+        w.bhi[4 * q] = h.x, w.bhi[4 * q + 1] = h.y, w.bhi[4 * q + 2] = h.z, w.bhi[4 * q + 3] = h.w;
+        w.blo[4 * q] = l.x, w.blo[4 * q + 1] = l.y, w.blo[4 * q + 2] = l.z, w.blo[4 * q + 3] = l.w;
+    }
+    w.w0 = __builtin_amdgcn_raw_buffer_load_b32(rs.r, hi ? rs.lane_off : kOff, 0, 0);
+}
+
+// Take all window words now (one vmcnt(#younger ops) wait on a single path):
+// words never read would otherwise stay "pending" for the compiler, and every
+// later reuse of their registers would wait vmcnt(0), draining the step's
+// early stores.
+__device__ __forceinline__ void mt_win_consume(const MtWin &w) {
+    asm volatile("" ::"v"(w.a[0]), "v"(w.a[1]), "v"(w.a[2]), "v"(w.a[3]), "v"(w.a[4]), "v"(w.a[5]),
+                 "v"(w.a[6]), "v"(w.a[7]), "v"(w.a[8]), "v"(w.a[9]), "v"(w.a[10]), "v"(w.a[11]));
+    asm volatile("" ::"v"(w.bhi[0]), "v"(w.bhi[1]), "v"(w.bhi[2]), "v"(w.bhi[3]), "v"(w.bhi[4]),
+                 "v"(w.bhi[5]), "v"(w.bhi[6]), "v"(w.bhi[7]), "v"(w.w0));
+    asm volatile("" ::"v"(w.blo[0]), "v"(w.blo[1]), "v"(w.blo[2]), "v"(w.blo[3]), "v"(w.blo[4]),
+                 "v"(w.blo[5]), "v"(w.blo[6]), "v"(w.blo[7]));
+}
+
+// The window's words of the current generation (word[j] = mt[idx + j]); those
+// at or past m are materialized and written back (buffer stores: masked-off
+// words go out of range), and m advances past the window.  Branch-free: the
+// recurrence is evaluated for all 8 words and masked in.
+__device__ __forceinline__ void mt_win_resolve(const MtRes &rs, int idx, int &m, bool want,
+                                               const MtWin &w, uint32_t (&word)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int k = idx + j;
+        const uint32_t x = k < 227 ? w.bhi[j] : w.blo[j];
+        const uint32_t b = k == kMtN - 1 ? w.w0 : w.a[j + 1];
+        const uint32_t f = 0u - (uint32_t)(k >= m);
+#ifdef ST_AB_NOMIX
+        word[j] = w.a[j] ^ (x & f);
+#else
+        word[j] = w.a[j] ^ ((x ^ mt_mix(w.a[j], b) ^ w.a[j]) & f);
+#endif
+#ifdef ST_AB_NOSTORE
+        const bool st = false;
+#else
+        const bool st = want && k >= m && k < kMtN;
+#endif
+        __builtin_amdgcn_raw_buffer_store_b32(word[j], rs.r, st ? rs.lane_off + 4u * (uint32_t)k : kOff, 0, 0);
+    }
+    if (want && idx + 8 > m) m = idx + 8 < kMtN ? idx + 8 : kMtN;
+}
+
+// _choose_shape (tetris_env.py:183-191) + the count update of _new_piece
+// (:199) for every lane with `need`: randint(1, sum(m)) = 1 + _randbelow(n)
+// with rejection sampling on getrandbits(k) (Lib/random.py:239-249).  `mtst`
+// is the lane's packed MT index (see mt_pack).  Wave-uniform: every lane of
+// the wave calls it.  `pre`: the window the caller loaded for lanes with
+// `have_pre` (at the index mt_begin gives).  The common case is branch-free:
+// all 8 words tempered as independent chains, each lane takes its first
+// accepted one; lanes the window does not settle (8 rejections, p <= 2^-8)
+// load the next window in the loop.
+__device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t &mtst,
+                                          uint32_t *mt_wave, int lane, const MtWin &pre,
+                                          bool have_pre) {
+    int32_t maxc = cnt[0], sumc = cnt[0];
+#pragma unroll
+    for (int i = 1; i < 7; ++i) {
+        maxc = cnt[i] > maxc ? cnt[i] : maxc;
+        sumc += cnt[i];
+    }
+    const uint32_t n = (uint32_t)(35 + 7 * maxc - sumc);
+    const int kb = 32 - __builtin_clz(n);
+    const MtRes rs = mt_res(mt_wave, lane);
+    int idx, m;
+    mt_unpack(mtst, idx, m);
+    if (need) mt_begin(idx, m);
+    bool pending = need;
+    uint32_t r = 0;
+    mt_win_consume(pre);
+    uint32_t word[8];
+    if (have_pre && pending) {
+        mt_win_resolve(rs, idx, m, true, pre, word);
+        int first = 8;
+        uint32_t rr = 0;
+#pragma unroll
+        for (int j = 7; j >= 0; --j) {
+            const uint32_t y = mt_temper(word[j]) >> (32 - kb);
+            const bool acc = y < n && idx + j < kMtN;
+            first = acc ? j : first;
+            rr = acc ? y : rr;
+        }
+        if (first < 8) {
+            pending = false;
+            r = rr;
+            idx += first + 1;
+        } else {
+            idx = idx + 8 < kMtN ? idx + 8 : kMtN;
+        }
+    }
+    while (__ballot(pending)) {
+        if (pending) mt_begin(idx, m);
+        MtWin w;
+        mt_win_load(rs, idx, m, pending, w);
+        mt_win_consume(w);
+        mt_win_resolve(rs, idx, m, pending, w, word);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (!__ballot(pending && idx < kMtN)) break;
+            if (pending && idx < kMtN) {
+                const uint32_t y = mt_temper(word[j]) >> (32 - kb);
+                ++idx;
+                if (y < n) {
+                    pending = false;
+                    r = y;
+                }
+            }
+        }
+    }
+    if (need) mtst = mt_pack(idx, m);
+    if (!need) return 0;
+    int32_t rr = (int32_t)r + 1;
+    int pick = 6;
+    bool found = false;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        rr -= 5 + maxc - cnt[i];
+        if (!found && rr <= 0) {
+            pick = i;
+            found = true;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 7; ++i) cnt[i] += (i == pick);
+    return pick;
+}
+
+// Complete a pending generation of ONE env (st_mt_sync): words [m, 624) by
+// the chunked recurrence, wave-cooperatively (all 64 lanes, wave-uniform m):
+// [0,227) reads old words | [227,454) reads [0,227) | [454,623) reads
+// [227,396) | 623 reads 396 and 0 -- each chunk only reads words that are
+// old or finished.
+__device__ void coop_complete(uint32_t *g, uint32_t *S, int lane, int m) {
     {
         uint32_t t[10];  // 624 = 9 * 64 + 48: issue all ten loads before any wait
 #pragma unroll
@@ -235,333 +445,29 @@ __device__ __noinline__ void coop_twist(uint32_t *g, uint32_t *S, int lane) {
             if (i < kMtN) S[i] = t[q];
         }
     }
-    __syncthreads();
+    wave_sync();
     uint32_t v[4];
+    auto chunk = [&](int lo, int hi, int xoff) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int k = lane + kWave * q;
-        if (k < 227) v[q] = S[k + 397] ^ mt_mix(S[k], S[k + 1]);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int k = lane + kWave * q;
-        if (k < 227) S[k] = v[q];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int k = 227 + lane + kWave * q;
-        if (k < 454) v[q] = S[k - 227] ^ mt_mix(S[k], S[k + 1]);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int k = 227 + lane + kWave * q;
-        if (k < 454) S[k] = v[q];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-        const int k = 454 + lane + kWave * q;
-        if (k < 623) v[q] = S[k - 227] ^ mt_mix(S[k], S[k + 1]);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-        const int k = 454 + lane + kWave * q;
-        if (k < 623) S[k] = v[q];
-    }
-    __syncthreads();
-    if (lane == 0) S[623] = S[396] ^ mt_mix(S[623], S[0]);
-    __syncthreads();
-    for (int i = lane; i < kMtN; i += kWave) g[i] = S[i];
-}
-
-// _choose_shape (tetris_env.py:183-191) + the count update of _new_piece
-// (:199) for every lane with `need`.  randint(1, sum(m)) = 1 + _randbelow(n)
-// with rejection sampling on getrandbits(k) (Lib/random.py:239-249).
-// Wave-uniform: every lane of the wave must call it.  Each round reads up to 8
-// consecutive words per lane (one or two 64-B lines of the env's MT block);
-// lanes whose state is exhausted are twisted cooperatively first.
-// Issue the loads of the next 8 MT words of this lane's stream (used by the
-// step kernel as soon as it knows the lane locks, so the round trip overlaps
-// the lock-path work).
-__device__ __forceinline__ void prefetch_words(const uint32_t *g, int32_t mtidx, bool want,
-                                               uint32_t (&w)[8]) {
-    // one exec region; words past index 623 are read but never consumed
-#pragma unroll
-    for (int j = 0; j < 8; ++j) w[j] = 0u;
-    if (want) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            w[j] = g[mtidx + j];  // cached (nt: packed rollout -12%); reads past the env's
-                                  // state land in the next env's or the allocation's 8-word pad
-    }
-}
-
-__device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], int32_t &mtidx,
-                                          uint32_t *mt_wave, uint32_t *S, int lane, bool twist,
-                                          const uint32_t (&pre)[8], bool have_pre) {
-    int32_t maxc = cnt[0], sumc = cnt[0];
-#pragma unroll
-    for (int i = 1; i < 7; ++i) {
-        maxc = cnt[i] > maxc ? cnt[i] : maxc;
-        sumc += cnt[i];
-    }
-    const uint32_t n = (uint32_t)(35 + 7 * maxc - sumc);
-    const int k = 32 - __builtin_clz(n);
-    uint32_t *g = mt_wave + (size_t)lane * kMtN;
-    bool pending = need;
-    bool fresh = false;  // state twisted (and stored) by this wave in this launch
-    uint32_t r = 0;
-    // Take all 8 prefetched words here (one vmcnt(#younger ops) wait on the
-    // loop's single entry path).  Words the loop never reads would otherwise
-    // stay "pending" for the compiler, and every later reuse of their
-    // registers would wait vmcnt(0) -- draining the caller's early stores.
-    asm volatile("" ::"v"(pre[0]), "v"(pre[1]), "v"(pre[2]), "v"(pre[3]), "v"(pre[4]), "v"(pre[5]),
-                 "v"(pre[6]), "v"(pre[7]));
-    // Fast path, branch-free: temper all 8 prefetched words (independent
-    // chains) and take each lane's first accepted one.  Lanes it does not
-    // settle (8 rejections, p <= 2^-8, or the state's end: a twist) continue
-    // in the loop below past the 8 words.
-    if (have_pre && pending && mtidx < kMtN) {
-        int first = 8;
-        uint32_t rr = 0;
-#pragma unroll
-        for (int j = 7; j >= 0; --j) {
-            const uint32_t y = mt_temper(pre[j]) >> (32 - k);
-            const bool acc = y < n && mtidx + j < kMtN;
-            first = acc ? j : first;
-            rr = acc ? y : rr;
+        for (int q = 0; q < 4; ++q) {
+            const int k = lo + lane + kWave * q;
+            if (k < hi && k >= m) v[q] = S[k + xoff] ^ mt_mix(S[k], S[k + 1]);
         }
-        if (first < 8) {
-            pending = false;
-            r = rr;
-            mtidx += first + 1;
-        } else {
-            mtidx = mtidx + 8 < kMtN ? mtidx + 8 : kMtN;
+        wave_sync();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = lo + lane + kWave * q;
+            if (k < hi && k >= m) S[k] = v[q];
         }
-    }
-    uint32_t w[8];
-    bool have = false;
-    while (__ballot(pending)) {
-        if (!twist && pending && mtidx >= kMtN) mtidx = 0;  // ablation: skip the twist
-        uint64_t tw = __ballot(pending && mtidx >= kMtN);
-        if (tw) {
-            bool mine = false;  // this lane's state was twisted in this round
-            do {
-                const int l = __builtin_ctzll(tw);
-                tw &= tw - 1;
-                coop_twist(mt_wave + (size_t)l * kMtN, S, lane);
-                if (lane == l) {  // the twisted lane takes its first words from LDS
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) w[j] = S[j];
-                    mine = true;
-                }
-                __syncthreads();  // S is reused by the next lane's twist
-            } while (tw);
-            if (mine) {
-                have = true;
-                mtidx = 0;
-                fresh = true;
-            }
-        }
-        if (pending && !have) {
-            // A state twisted in this launch is re-read from global memory only
-            // if one draw needs more than 8 of its words (p ~ 1e-3): drain our
-            // stores to L2 first; the nt loads bypass the (stale) L1.
-            if (__ballot(pending && fresh)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                w[j] = __builtin_nontemporal_load(g + (mtidx + j < kMtN ? mtidx + j : kMtN - 1));
-            asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]),
-                         "v"(w[6]), "v"(w[7]));  // see above: no loads left pending
-        }
-        // consume words until every lane has its piece (most waves stop after
-        // 3-5 of the 8: each getrandbits(k) is accepted with p >= 1/2)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            if (!__ballot(pending && mtidx < kMtN)) break;
-            if (pending && mtidx < kMtN) {
-                const uint32_t y = mt_temper(w[j]) >> (32 - k);
-                ++mtidx;
-                if (y < n) {
-                    pending = false;
-                    r = y;
-                }
-            }
-        }
-        have = false;
-    }
-    if (!need) return 0;
-    int32_t rr = (int32_t)r + 1;
-    int pick = 6;
-    bool found = false;
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-        rr -= 5 + maxc - cnt[i];
-        if (!found && rr <= 0) {
-            pick = i;
-            found = true;
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 7; ++i) cnt[i] += (i == pick);
-    return pick;
-}
-
-// ---------------------------------------------------------------- MT word ring
-// st_rollout keeps each lane's upcoming MT words in LDS: ring slot s of lane l
-// is R[s * 64 + l] and holds word index i at s = i & 31 for i in [mtidx, hi).
-// Refills fetch the aligned 16-word chunk at `hi` (64 B, one cache line) with
-// one nt dwordx4 load per 4 words, a step before the words can be needed, and
-// are committed into the ring at the next draw -- so draws need no dependent
-// load and each line of MT state is fetched once.
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-struct MtRing {
-    int32_t hi;       // ring holds the words with index < hi (>= mtidx unconsumed)
-    int32_t pend_lo;  // start index of the refill in flight, -1 if none
-    u32x4 pend[4];
-};
-
-__device__ __forceinline__ void ring_put(uint32_t *R, int lane, int idx, uint32_t w) {
-    R[(idx & 31) * kWave + lane] = w;
-}
-
-__device__ __forceinline__ void ring_init(MtRing &r, uint32_t *R, const uint32_t *g, int32_t mtidx,
-                                          int lane) {
-    const int lo = mtidx & ~15;  // 624 = 39 * 16: chunks never straddle the end
-    const int nfill = kMtN - lo < 32 ? kMtN - lo : 32;  // 0, 16 or 32 words
-    uint4 v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-        v[j] = 4 * j < nfill ? *reinterpret_cast<const uint4 *>(g + lo + 4 * j) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        if (4 * j < nfill) {
-            ring_put(R, lane, lo + 4 * j, v[j].x);
-            ring_put(R, lane, lo + 4 * j + 1, v[j].y);
-            ring_put(R, lane, lo + 4 * j + 2, v[j].z);
-            ring_put(R, lane, lo + 4 * j + 3, v[j].w);
-        }
-    }
-    r.hi = lo + nfill;
-    r.pend_lo = -1;
-}
-
-// After a draw: start fetching the next chunk once <= 16 words remain.
-__device__ __forceinline__ void ring_refill(MtRing &r, const uint32_t *g, int32_t mtidx) {
-    if (mtidx > r.hi) r.hi = mtidx & ~15;  // a draw ran past the ring (fallback loads)
-    if (r.pend_lo < 0 && r.hi < kMtN && r.hi - mtidx <= 16) {
-        r.pend_lo = r.hi;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            r.pend[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(g + r.hi + 4 * j));
-    }
-}
-
-__device__ __forceinline__ void ring_commit(MtRing &r, uint32_t *R, int lane) {
-    if (r.pend_lo >= 0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            ring_put(R, lane, r.pend_lo + 4 * j, r.pend[j].x);
-            ring_put(R, lane, r.pend_lo + 4 * j + 1, r.pend[j].y);
-            ring_put(R, lane, r.pend_lo + 4 * j + 2, r.pend[j].z);
-            ring_put(R, lane, r.pend_lo + 4 * j + 3, r.pend[j].w);
-        }
-        r.hi = r.pend_lo + 16;
-        r.pend_lo = -1;
-    }
-}
-
-// draw_shape with the words taken from the ring (see draw_shape for the
-// algorithm).  Words past the ring (a single draw consuming > 16 words) are
-// loaded directly; exhausted states are twisted cooperatively and the
-// twisted lane refills its ring from the new state in LDS.
-__device__ __forceinline__ int draw_shape_ring(bool need, int32_t (&cnt)[7], int32_t &mtidx,
-                                               uint32_t *mt_wave, uint32_t *S, uint32_t *R,
-                                               MtRing &ring, int lane, bool twist) {
-    ring_commit(ring, R, lane);
-    int32_t maxc = cnt[0], sumc = cnt[0];
-#pragma unroll
-    for (int i = 1; i < 7; ++i) {
-        maxc = cnt[i] > maxc ? cnt[i] : maxc;
-        sumc += cnt[i];
-    }
-    const uint32_t n = (uint32_t)(35 + 7 * maxc - sumc);
-    const int k = 32 - __builtin_clz(n);
-    const uint32_t *g = mt_wave + (size_t)lane * kMtN;
-    bool pending = need;
-    uint32_t r = 0;
-    while (__ballot(pending)) {
-        if (!twist && pending && mtidx >= kMtN) mtidx = 0;  // ablation: skip the twist
-        uint64_t tw = __ballot(pending && mtidx >= kMtN);
-        if (tw) {
-            bool mine = false;
-            do {
-                const int l = __builtin_ctzll(tw);
-                tw &= tw - 1;
-                coop_twist(mt_wave + (size_t)l * kMtN, S, lane);
-                if (lane == l) {
-#pragma unroll 4
-                    for (int i = 0; i < 32; ++i) ring_put(R, lane, i, S[i]);
-                    mine = true;
-                }
-                __syncthreads();  // S is reused by the next lane's twist
-            } while (tw);
-            // the twist's stores must reach L2 before any nt reload of them
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (mine) {
-                mtidx = 0;
-                ring.hi = 32;
-                ring.pend_lo = -1;
-            }
-        }
-        uint32_t w[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int idx = mtidx + j;
-            w[j] = idx < ring.hi ? R[(idx & 31) * kWave + lane] : 0u;
-        }
-        if (__ballot(pending && mtidx + 8 > ring.hi && ring.hi < kMtN)) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int idx = mtidx + j;
-                if (pending && idx >= ring.hi && idx < kMtN) w[j] = __builtin_nontemporal_load(g + idx);
-            }
-        }
-        // consume words until every lane has its piece (most waves stop after
-        // 3-5 of the 8: each getrandbits(k) is accepted with p >= 1/2)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            if (!__ballot(pending && mtidx < kMtN)) break;
-            if (pending && mtidx < kMtN) {
-                const uint32_t y = mt_temper(w[j]) >> (32 - k);
-                ++mtidx;
-                if (y < n) {
-                    pending = false;
-                    r = y;
-                }
-            }
-        }
-    }
-    if (!need) return 0;
-    int32_t rr = (int32_t)r + 1;
-    int pick = 6;
-    bool found = false;
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-        rr -= 5 + maxc - cnt[i];
-        if (!found && rr <= 0) {
-            pick = i;
-            found = true;
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 7; ++i) cnt[i] += (i == pick);
-    return pick;
+        wave_sync();
+    };
+    chunk(0, 227, 397);
+    chunk(227, 454, -227);
+    chunk(454, 623, -227);
+    if (lane == 0 && m <= 623) S[623] = S[396] ^ mt_mix(S[623], S[0]);
+    wave_sync();
+    for (int i = lane; i < kMtN; i += kWave)
+        if (i >= m) g[i] = S[i];
 }
 
 __device__ __forceinline__ uint32_t pack_piece(int id, int rot, int ax, int ay, int lock) {
@@ -587,16 +493,16 @@ __device__ __forceinline__ uint32_t pack_piece(int id, int rot, int ax, int ay, 
 template <int WT, int HT, bool F32, bool STAMP, int KSTEPS>
 __device__ __forceinline__ void run_steps(const KParams &p) {
     [[maybe_unused]] uint64_t tstamp[10] = {};
+    [[maybe_unused]] uint64_t draw_kind = 0;  // stamp build: 1 = a lane twisted, 2 = a draw ran past 8 words
     constexpr bool S32 = HT != 0 && HT <= 25;  // see pc_bits
     [[maybe_unused]] uint64_t rt0 = 0;
     if constexpr (STAMP) rt0 = __builtin_amdgcn_s_memrealtime();
     ST_STAMP(0);
     // LDS: board columns L[x + kPad][lane] (walls at both ends), the staged
-    // counter rows SS[r][lane] (r < 14: stats rows, 14: piece word), the MT
-    // twist scratch and the piece table.
+    // counter rows SS[r][lane] (r < 14: stats rows, 14: piece word) and the
+    // piece table.
     __shared__ __attribute__((aligned(16))) uint32_t L[(kMaxW + 2 * kPad) * kWave];
     __shared__ __attribute__((aligned(16))) uint32_t SS[kHotQ * 4 * kWave];
-    __shared__ uint32_t S[kMtN];
     __shared__ uint2 T2[28];
     // st_step: per env board keep-mask, changed board columns, changed counter rows
     __shared__ __attribute__((aligned(16))) uint32_t KM[KSTEPS == 1 ? kWave : 4];
@@ -606,7 +512,6 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     // free transposed reads) and the 16 float4 patterns of a 4-bit nibble.
     __shared__ uint32_t O[F32 ? kWave * (kMaxW + 1) : 1];
     __shared__ __attribute__((aligned(16))) float4 F4[F32 ? 16 : 1];
-    __shared__ uint32_t R[(KSTEPS != 1 && F32 && ST_RING) ? 32 * kWave : 1];  // MT word ring
     const int W = WT ? WT : p.W;
     const int H = HT ? HT : p.H;
     const int lane = threadIdx.x;
@@ -654,9 +559,6 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     // gets sunk by the compiler past the state loads' completion -- one more
     // serialized round trip -- and inline asm here makes the register
     // allocator spill the in-flight state loads to scratch).
-#if defined(ST_AB_TAB_LOAD) && ST_AB_TAB_LOAD
-    const uint32_t tab_m = c_tab_m[lane < 28 ? lane : 0], tab_g = c_tab_g[lane < 28 ? lane : 0];
-#else
     uint32_t tab_m = 0, tab_g = 0;
 #pragma unroll
     for (int i = 0; i < 28; ++i) {
@@ -664,7 +566,6 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         tab_m = me ? kTab.m[i] : tab_m;
         tab_g = me ? kTab.g[i] : tab_g;
     }
-#endif
     const uint32_t floor_op = floorb;
     const int lrow = lane >> 4, lcc = 4 * (lane & 15);  // this lane's row-in-group, env slot
 #pragma unroll
@@ -692,12 +593,8 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
             F4[lane] = make_float4((float)(lane & 1), (float)((lane >> 1) & 1),
                                    (float)((lane >> 2) & 1), (float)((lane >> 3) & 1));
     }
-    __syncthreads();
+    wave_sync();
     auto ss = [&](int r) -> uint32_t & { return SS[r * kWave + lane]; };
-    [[maybe_unused]] MtRing ring;
-    // ring only where it pays (A/B): the HBM-bound f32 rollout
-    constexpr bool kRing = KSTEPS != 1 && F32 && ST_RING;
-    if constexpr (kRing) ring_init(ring, R, p.mt + e * kMtN, (int32_t)ss(ST_STAT_MT_INDEX), lane);
 
     for (int t = 0; t < K; ++t) {
     const uint32_t act = real ? act_next : 6u;
@@ -756,12 +653,18 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         locknow = lock == 0 && !(p.ablate & 1u);
     }
     ST_STAMP(2);
-    // MT words for the piece this lock will draw: issue now, consume after the
-    // lock path (every locking lane draws: a spawn, or the same-step reset's).
-    int32_t mtidx = (int32_t)ss(ST_STAT_MT_INDEX);
-    uint32_t pre[8];
-    const bool want_pre = !kRing && locknow && mtidx < kMtN && !(p.ablate & 2u);
-    if constexpr (!kRing) prefetch_words(p.mt + e * kMtN, mtidx, want_pre, pre);
+    // MT window for the piece this lock will draw: issued now, consumed after
+    // the lock path (every locking lane draws: a spawn, or the same-step
+    // reset's).  mt_begin only positions the window; the draw commits.
+    uint32_t mtst = ss(ST_STAT_MT_INDEX);  // packed (mt_pack)
+    const bool want_pre = locknow && !(p.ablate & 2u);
+    MtWin pre;
+    {
+        int pidx, pm;
+        mt_unpack(mtst, pidx, pm);
+        mt_begin(pidx, pm);
+        mt_win_load(mt_res(p.mt + e0 * kMtN, lane), pidx, pm, want_pre, pre);
+    }
 
     // ---- lock path (tetris_env.py:263-299) ----
     bool died = false, spawn = false;
@@ -871,7 +774,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         if (died) bdirty = ~0u;
         KM[lane] = reset_now ? 0u : hmask;
         BD[lane] = bdirty;
-        __syncthreads();
+        wave_sync();
         const uint4 km = *reinterpret_cast<const uint4 *>(&KM[lcc]);
         const uint4 bd4 = *reinterpret_cast<const uint4 *>(&BD[lcc]);
         const uint32_t bdl = (bd4.x | bd4.y | bd4.z | bd4.w) >> lrow;
@@ -895,7 +798,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
                 buf_store16(rb, dirty ? boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff, v);
             }
         }
-        __syncthreads();  // the board reads above precede the overlay paint
+        wave_sync();  // the board reads above precede the overlay paint
         if (!spawn) paint<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
     }
 
@@ -905,21 +808,17 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
 #pragma unroll
     for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)ss(ST_STAT_COUNT0 + i);  // used by drawing lanes only
     int pick = 0;
+    [[maybe_unused]] const uint32_t mt_before = mtst;
     if constexpr (STAMP) {  // diagnostic split of the draw: MT-word wait | compute
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         ST_STAMP(9);
     }
-    if (!(p.ablate & 2u)) {
-        if constexpr (!kRing) {
-            pick = draw_shape(draw, cnt, mtidx, p.mt + e0 * kMtN, S, lane, !(p.ablate & 4u), pre,
-                              want_pre);
-        } else {
-            pick = draw_shape_ring(draw, cnt, mtidx, p.mt + e0 * kMtN, S, R, ring, lane,
-                                   !(p.ablate & 4u));
-            ring_refill(ring, p.mt + e * kMtN, mtidx);
-        }
-    }
+    if (!(p.ablate & 2u)) pick = draw_shape(draw, cnt, mtst, p.mt + e0 * kMtN, lane, pre, want_pre);
     ST_STAMP(4);
+    if constexpr (STAMP) {  // 1: a draw started a generation, 2: a draw ran past its 8 words
+        const int i0 = (int)(mt_before & 0xFFFFu), i1 = (int)(mtst & 0xFFFFu);
+        draw_kind = (__ballot(draw && i1 < i0) ? 1u : 0u) | (__ballot(draw && i1 >= i0 && i1 - i0 > 8) ? 2u : 0u);
+    }
     uint2 odesc = desc;
     int oax = ax, oay = ay;
     uint32_t pw_out = pack_piece(id, rot, ax, ay, lock);
@@ -953,7 +852,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         put(ST_STAT_HOLES, holes);
         put(ST_STAT_PIECE_HEIGHT, height);
         put(ST_STAT_DEATHS, deaths);
-        put(ST_STAT_MT_INDEX, mtidx);
+        put(ST_STAT_MT_INDEX, (int32_t)mtst);
         if (draw) {
             atomicAdd(&ss(ST_STAT_COUNT0 + pick), 1u);  // shape_counts[name] += 1, :199 (ds_add, no return)
             sdirty |= 1u << (ST_STAT_COUNT0 + pick);
@@ -963,7 +862,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
 
     // ---- observation (tetris_env.py:301-302): board + current piece ----
     if (KSTEPS != 1 || spawn) paint<S32>(L, lane, odesc.x, odesc.y, oax, oay, hmask);
-    __syncthreads();
+    wave_sync();
     const bool wide_obs = (p.n & 3) == 0 && e0 + kWave <= p.n &&
                           (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0;
     if (obs_t && !(p.ablate & 8u)) {
@@ -998,7 +897,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
             constexpr int CPC = HT / 4, CPE = WT * CPC;
 #pragma unroll
             for (int x = 0; x < WT; ++x) O[lane * (WT + 1) + x] = lcol(L, x, lane) & hmask;
-            __syncthreads();
+            wave_sync();
             float4 *out4 = reinterpret_cast<float4 *>(out);
             const int total = nreal * CPE;
             for (int c = lane; c < total; c += kWave) {
@@ -1028,13 +927,13 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         // Erasing the overlaid piece yields the post-step board for every
         // lane: non-locking lanes and spawns (overlay cells were empty), and a
         // death without auto-reset (R8: _set_piece(False), tetris_env.py:303).
-        __syncthreads();
+        wave_sync();
         erase<S32>(L, lane, odesc.x, odesc.y, oax, oay, hmask);
         if (reset_now)
             for (int x = 0; x < W; ++x) lcol(L, x, lane) = floorb;
     }
     }  // for t
-    __syncthreads();
+    wave_sync();
     if constexpr (KSTEPS != 1) {
         uint32_t *bdst = p.board + e0;
 #pragma unroll
@@ -1076,6 +975,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
             p.stamps[blockIdx.x * kStampWords + 11] = __builtin_amdgcn_s_memrealtime();
             p.stamps[blockIdx.x * kStampWords + 12] = __builtin_amdgcn_s_getreg(0xF804);  // HW_ID
             p.stamps[blockIdx.x * kStampWords + 13] = __builtin_amdgcn_s_getreg(0xF814);  // XCC_ID
+            p.stamps[blockIdx.x * kStampWords + 14] = draw_kind;
         }
     }
 }
@@ -1094,7 +994,6 @@ __global__ __launch_bounds__(kWave) void k_rollout(KParams p) {
 // TetrisEngine.clear (tetris_env.py:306-315) on masked envs.  n_deaths,
 // shape_counts and the lock-delay counter persist (R15).
 __global__ __launch_bounds__(kWave) void k_reset(KParams p) {
-    __shared__ uint32_t S[kMtN];
     const int lane = threadIdx.x;
     const int64_t e0 = (int64_t)blockIdx.x * kWave;
     const int64_t e = e0 + lane;
@@ -1104,17 +1003,17 @@ __global__ __launch_bounds__(kWave) void k_reset(KParams p) {
     int32_t cnt[7];
 #pragma unroll
     for (int i = 0; i < 7; ++i) cnt[i] = st[(ST_STAT_COUNT0 + i) * sd];
-    int32_t mtidx = st[ST_STAT_MT_INDEX * sd];
+    uint32_t mtst = (uint32_t)st[ST_STAT_MT_INDEX * sd];
     const uint32_t pw = p.piece[e];
-    const uint32_t nopre[8] = {};
-    const int pick = draw_shape(m, cnt, mtidx, p.mt + e0 * kMtN, S, lane, true, nopre, false);
+    const MtWin nopre{};
+    const int pick = draw_shape(m, cnt, mtst, p.mt + e0 * kMtN, lane, nopre, false);
     if (m) {
         st[ST_STAT_TIME * sd] = 0;
         st[ST_STAT_SCORE * sd] = 0;
         st[ST_STAT_HOLES * sd] = 0;
         st[ST_STAT_LINES * sd] = 0;
         st[ST_STAT_PIECE_HEIGHT * sd] = 0;
-        st[ST_STAT_MT_INDEX * sd] = mtidx;
+        st[ST_STAT_MT_INDEX * sd] = (int32_t)mtst;
 #pragma unroll
         for (int i = 0; i < 7; ++i) st[(ST_STAT_COUNT0 + i) * sd] = cnt[i];
         for (int x = 0; x < p.W; ++x) p.board[x * sd + e] = 0u;
@@ -1178,6 +1077,28 @@ __global__ void k_seed(KParams p) {
     st[ST_STAT_MT_INDEX * sd] = 0;
     for (int x = 0; x < p.W; ++x) p.board[x * sd + e] = 0u;
     p.piece[e] = pack_piece(0, 0, p.W / 2, 0, 0);
+}
+
+// ---------------------------------------------------------------- MT sync
+// st_mt_sync: finish every generation the draws left in progress (M != 0), so
+// that stats/mt hold CPython's state again.  One wave per 64 envs; the wave
+// completes its pending lanes' states one after another, cooperatively.
+__global__ __launch_bounds__(kWave) void k_mt_sync(KParams p) {
+    __shared__ uint32_t S[kMtN];
+    const int lane = threadIdx.x;
+    const int64_t e0 = (int64_t)blockIdx.x * kWave;
+    const int64_t e = e0 + lane;
+    int32_t *row = p.stats + (int64_t)ST_STAT_MT_INDEX * p.stride;
+    const uint32_t r = (uint32_t)row[e];
+    uint64_t pend = __ballot((r >> 16) != 0u);
+    while (pend) {
+        const int l = __builtin_ctzll(pend);
+        pend &= pend - 1;
+        const uint32_t rl = __shfl(r, l);
+        coop_complete(p.mt + (e0 + l) * kMtN, S, lane, (int)(rl >> 16) - 1);
+        wave_sync();
+    }
+    if ((r >> 16) != 0u) row[e] = (int32_t)(r & 0xFFFFu);
 }
 
 // ---------------------------------------------------------------- render
@@ -1292,6 +1213,11 @@ hipError_t launch_step(const KParams &p, hipStream_t s) {
         if (f32) hipLaunchKernelGGL((k_step<0, 0, true>), grid, block, 0, s, p);
         else hipLaunchKernelGGL((k_step<0, 0, false>), grid, block, 0, s, p);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_mt_sync(const KParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(k_mt_sync, dim3((unsigned)(p.stride / kWave)), dim3(kWave), 0, s, p);
     return hipGetLastError();
 }
 

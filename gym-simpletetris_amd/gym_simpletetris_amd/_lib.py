@@ -36,7 +36,7 @@ NSTAT = 19
 MT_N = 624
 
 EXPORTS = ("st_create", "st_destroy", "st_seed", "st_reset", "st_step", "st_step_f32", "st_rollout",
-           "st_obs_to_f32", "st_render", "st_grayscale", "st_state", "st_copy", "st_state_bytes", "st_save",
+           "st_obs_to_f32", "st_render", "st_grayscale", "st_state", "st_copy", "st_mt_sync", "st_state_bytes", "st_save",
            "st_load", "st_gen_actions", "st_debug_stamps", "st_last_error", "st_abi_version")
 
 
@@ -88,6 +88,7 @@ def load(path: str = LIB_PATH):
         "st_grayscale": ([vp, vp, i32, i32, i32, vp, vp], ctypes.c_int),
         "st_state": ([vp, ctypes.POINTER(StateViews)], ctypes.c_int),
         "st_copy": ([vp, vp, i64, vp], ctypes.c_int),
+        "st_mt_sync": ([vp, vp], ctypes.c_int),
         "st_state_bytes": ([vp], i64),
         "st_save": ([vp, vp, i64], ctypes.c_int),
         "st_load": ([vp, vp, i64], ctypes.c_int),

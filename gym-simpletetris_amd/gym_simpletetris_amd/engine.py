@@ -216,9 +216,19 @@ class TetrisBatch:
     def _view_ptr(self, name):
         return getattr(self._views, name)
 
+    def sync_mt(self):
+        """Complete the generations the lazy in-kernel MT twist left in
+        progress (st_mt_sync): afterwards stats/mt hold CPython's state."""
+        if not hasattr(self._L, "st_mt_sync"):  # only an ST_LIB A/B build predating it
+            return
+        with torch.cuda.device(self.device):
+            C.check(self._L.st_mt_sync(self._ctx, self._stream()))
+
     def state_tensors(self, fields=("board", "piece", "stats")) -> dict:
         """Device copies of the state (full stride; slice [..., :n] for real envs)."""
         out = {}
+        if "stats" in fields or "mt" in fields:
+            self.sync_mt()
         with torch.cuda.device(self.device):
             for f in fields:
                 shape = self._sizes()[f]

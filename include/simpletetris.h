@@ -85,7 +85,7 @@ enum st_stat {
     ST_STAT_PIECE_HEIGHT = 4,
     ST_STAT_DEATHS = 5,
     ST_STAT_COUNT0 = 6,   /* shape_counts T,J,L,Z,S,I,O: rows 6..12 */
-    ST_STAT_MT_INDEX = 13,/* MT19937 index (0..624) */
+    ST_STAT_MT_INDEX = 13,/* MT19937 index (0..624); see st_mt_sync */
     ST_STAT_PIECE = 14,   /* the piece word (uint32, = st_state_views.piece) */
     ST_STAT_EP_TIME = 15, /* terminal counters of the last finished episode */
     ST_STAT_EP_SCORE = 16,/* (ST_AUTORESET_SAME_STEP only)                   */
@@ -180,6 +180,16 @@ int st_state(st_ctx *ctx, st_state_views *out);
 /* hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, stream) -- moves state
  * between the views above and caller buffers (crafted states). */
 int st_copy(void *dst, const void *src, int64_t bytes, st_stream stream);
+
+/* The step kernels twist each env's MT19937 state lazily: a draw computes
+ * only the words it reads, so between steps an env may hold a generation in
+ * progress, marked in ST_STAT_MT_INDEX (index | (m + 1) << 16: words [0, m)
+ * of the new generation, the rest of the old).  st_mt_sync completes those
+ * generations on `stream`, after which every env's mt words and index are
+ * exactly CPython's random.getstate() (index 0..624).  Call it before reading
+ * stats or mt through st_state's views; st_save calls it itself.  Writing a
+ * CPython state (index 0..624, no high bits) is always valid. */
+int st_mt_sync(st_ctx *ctx, st_stream stream);
 
 /* State snapshot: the engine attributes of every env (board, piece, counters,
  * shape counts: TetrisEngine.__init__ / _new_piece, tetris_env.py:138-199)

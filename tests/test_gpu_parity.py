@@ -410,6 +410,53 @@ def test_long_rejection_runs_and_twists(mode):
         assert np.array_equal(fin["mt"][i], np.ctypeslib.as_array(ob.envs[i].rng.mt)), i
 
 
+def test_lazy_twist_across_generations():
+    """Lock every step for ~2.5 MT generations: the in-kernel twist is lazy
+    (a draw materializes only its words), so states between steps hold
+    generations in progress; st_mt_sync must restore CPython's exact state at
+    any point, and syncing mid-run must not change what follows."""
+    import ctypes
+    from gym_simpletetris_amd import _lib as C
+    G = _engine()
+    n, T, chunk = 256, 1200, 100
+    seeds = [11 + e for e in range(n)]
+    a = G.TetrisBatch(n, autoreset="same_step", seeds=seeds)
+    b = G.TetrisBatch(n, autoreset="same_step", seeds=seeds)
+    a.reset()
+    b.reset()
+    ob = O.OracleBatch(n, seeds)
+    ob.reset()
+    acts = np.full((T, n), 2, np.uint8)              # hard drops: a draw every step
+    acts[::4] = O.splitmix64_actions(3, 0, T, n)[::4]
+    ref = ob.rollout(acts)
+    saw_lazy = False
+    for c0 in range(0, T, chunk):
+        da = torch.as_tensor(acts[c0:c0 + chunk], device=a.device)
+        oa, ra, _ = a.rollout(da)
+        for t in range(c0, c0 + chunk):
+            ob_, rb, _ = b.step(da[t - c0])
+            assert torch.equal(ob_, oa[t - c0]) and torch.equal(rb, ra[t - c0]), t
+        assert np.array_equal(ra.cpu().numpy(), ref["reward"][c0:c0 + chunk]), c0
+        assert np.array_equal(oa.cpu().numpy().view(np.uint32).transpose(0, 2, 1),
+                              ref["obs"][c0:c0 + chunk]), c0
+        # raw (unsynced) index row of b: some envs mid-generation
+        raw = torch.empty(b.stride, dtype=torch.int32, device=b.device)
+        v = b._views
+        C.check(b._L.st_copy(ctypes.c_void_p(raw.data_ptr()),
+                             ctypes.c_void_p(v.stats + C.STAT["mt_index"] * v.stride * 4),
+                             raw.numel() * 4, b._stream()))
+        saw_lazy |= bool(((raw[:n].cpu().numpy() >> 16) != 0).any())
+        if (c0 // chunk) % 3 == 1:
+            a.get_state(("mt", "stats"))                # sync a only, mid-run
+    assert saw_lazy
+    fa, fb = a.get_state(), b.get_state()
+    for k in fa:
+        assert np.array_equal(fa[k], fb[k]), k
+    for i in range(n):
+        assert int(fa["stats"][13, i]) == ob.envs[i].rng.index, i
+        assert np.array_equal(fa["mt"][i], np.ctypeslib.as_array(ob.envs[i].rng.mt)), i
+
+
 def test_abi_error_paths():
     """The C ABI rejects bad arguments and call-order violations with codes
     and a message instead of faulting (reference: exceptions)."""

@@ -22,14 +22,45 @@ buf = np.zeros(nw * W, np.uint64)
 rts = []
 names = ["loads", "action+drop", "lock path", "early stores", "store+MT wait", "draw", "obs (+f32) issue", "state stores issue", "store drain"]
 acc = []
-for t in range(300):
-    b.step(b.gen_actions(t, 0x5EED), obs="f32" if f32 else "packed")
-    if t >= 100:
-        b._L.st_debug_stamps(b._ctx, ctypes.c_void_p(buf.ctypes.data), buf.size)
-        full = buf.reshape(nw, W).astype(np.int64)
-        st = full[:, [0, 1, 2, 3, 8, 9, 4, 5, 6, 7]]  # stamps 8, 9 sit between 3 and 4
-        acc.append(np.diff(st, axis=1))
-        rts.append(full[:, 10:14].copy())
+
+
+def record():
+    b._L.st_debug_stamps(b._ctx, ctypes.c_void_p(buf.ctypes.data), buf.size)
+    full = buf.reshape(nw, W).astype(np.int64)
+    st = full[:, [0, 1, 2, 3, 8, 9, 4, 5, 6, 7]]  # stamps 8, 9 sit between 3 and 4
+    acc.append(np.diff(st, axis=1))
+    rts.append(full[:, 10:15].copy())
+
+
+if "--graph" in sys.argv:
+    # back-to-back launches as in bench.py: a hipGraph of 10 st_step calls,
+    # replayed; the stamps are those of each replay's last step
+    C = G._lib
+    s = torch.cuda.Stream()
+    acts = [b.gen_actions(t, 0x5EED).clone() for t in range(100 + 10 * 200)]
+    obs = torch.empty((b.width, n), dtype=torch.int32, device=b.device)
+    rew = torch.empty(n, dtype=torch.int32, device=b.device)
+    done = torch.empty(n, dtype=torch.uint8, device=b.device)
+    for t in range(100):
+        b.step(acts[t])
+    torch.cuda.synchronize()
+    vp = ctypes.c_void_p
+    sp = vp(s.cuda_stream)
+    for rep in range(200):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for t in range(100 + 10 * rep, 110 + 10 * rep):
+                C.check(b._L.st_step(b._ctx, vp(acts[t].data_ptr()), vp(obs.data_ptr()),
+                                     vp(rew.data_ptr()), vp(done.data_ptr()), sp))
+        g.replay()
+        torch.cuda.synchronize()
+        record()
+        del g
+else:
+    for t in range(300):
+        b.step(b.gen_actions(t, 0x5EED), obs="f32" if f32 else "packed")
+        if t >= 100:
+            record()
 a = np.concatenate(acc)
 tot = (a.sum(1))
 print(f"f32={f32} waves={nw} steps=200  total cycles median {np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} max {tot.max()}")
@@ -55,3 +86,24 @@ for k in range(8):
     m = xcc == k
     if m.any():
         print(f"  xcc {k}: start median {np.median(t0[:, m])*ns:.0f} end max {t1[:, m].max(1).mean()*ns:.0f}")
+
+# the slowest wave of each step (the kernel ends with it): which phase is long?
+life = a.reshape(len(acc), nw, -1)
+tot_w = life.sum(2)
+slow = np.argmax(tot_w, axis=1)
+sl = life[np.arange(len(acc)), slow]
+print("slowest wave per step, mean cycles by phase (vs the median wave):")
+for i, nm in enumerate(names):
+    print(f"  {nm:18s} slowest {sl[:, i].mean():8.0f}   median wave {np.median(life[:, :, i]):7.0f}")
+print(f"  {'total':18s} slowest {tot_w.max(1).mean():8.0f}   median wave {np.median(tot_w):7.0f}")
+k = 10
+top = np.sort(tot_w, axis=1)[:, -k:]
+print(f"the {k} slowest waves per step: mean total {top.mean():.0f} cycles")
+
+kind = r[:, :, 4]  # 1: a lane twisted its MT state, 2: a draw ran past the 8 prefetched words
+for kd, nm in ((0, "plain"), (1, "twist"), (2, "past 8 words"), (3, "both")):
+    m = kind == kd
+    if m.any():
+        print(f"draw kind {nm:13s}: {m.sum() / len(acc):6.1f} waves/step, draw phase median "
+              f"{np.median(life[:, :, 5][m]):6.0f}, total median {np.median(tot_w[m]):6.0f} cycles")
+print("kind of the slowest wave per step:", np.bincount(kind[np.arange(len(acc)), slow], minlength=4).tolist())
