@@ -111,7 +111,8 @@ def load_pmc(kernel_prefix: str):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--steps", type=int, default=4000,
+                    help="timed steps (default spans >= 2 MT generations of a typical env, ~1,650 steps each)")
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--n-envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c3")
@@ -184,7 +185,7 @@ def main():
     torch.cuda.synchronize(dev)
 
     def spawned():
-        st = eng.state_tensors(("stats",))["stats"][6:13, :n_local]
+        st = eng.state_tensors(("stats",), sync=False)["stats"][6:13, :n_local]
         return int(st.to(torch.int64).sum().item())
 
     def timed(run, nsteps):

@@ -22,7 +22,6 @@ struct st_ctx {
     uint32_t *piece;
     int32_t *stats;
     uint32_t *mt;
-    uint32_t *mt_alloc;  // mt - kMtPadFront
 };
 
 namespace {
@@ -82,10 +81,10 @@ st::KParams params(const st_ctx *c) {
 void free_state(st_ctx *c) {
     if (c->board) (void)hipFree(c->board);
     if (c->stats) (void)hipFree(c->stats);
-    if (c->mt_alloc) (void)hipFree(c->mt_alloc);
+    if (c->mt) (void)hipFree(c->mt);
     if (c->stamps) (void)hipFree(c->stamps);
     c->stamps = nullptr;
-    c->board = c->piece = c->mt = c->mt_alloc = nullptr;
+    c->board = c->piece = c->mt = nullptr;
     c->stats = nullptr;
 }
 
@@ -129,12 +128,8 @@ int st_create(st_ctx **out, const st_config *cfg, int device, int64_t n_envs) {
     if (e == hipSuccess) e = hipMalloc(&c->board, sd * wpad * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&c->stats, sd * ST_NSTAT * sizeof(int32_t));
     if (e == hipSuccess) c->piece = reinterpret_cast<uint32_t *>(c->stats) + ST_STAT_PIECE * sd;
-    // MT states with pads: a draw's window reads words idx-227.. and idx+397..
-    // of its own state unconditionally, which for the first / last env fall
-    // outside the states (values never used)
-    if (e == hipSuccess)
-        e = hipMalloc(&c->mt_alloc, (st::kMtPadFront + sd * st::kMtN + st::kMtPadBack) * sizeof(uint32_t));
-    if (e == hipSuccess) c->mt = c->mt_alloc + st::kMtPadFront;
+    // MT states: [stride][kMtPitch] (+ the back pad a draw window may reach)
+    if (e == hipSuccess) e = hipMalloc(&c->mt, (sd * st::kMtPitch + st::kMtPadBack) * sizeof(uint32_t));
     if (e == hipSuccess && getenv("ST_STAMPS"))
         e = hipMalloc(&c->stamps, (sd / st::kWave) * st::kStampWords * sizeof(uint64_t));
     if (e != hipSuccess) {
@@ -283,6 +278,7 @@ int st_state(st_ctx *c, st_state_views *out) {
     out->piece = c->piece;
     out->stats = c->stats;
     out->mt = c->mt;
+    out->mt_pitch = st::kMtPitch;
     out->n_envs = c->n;
     out->stride = c->stride;
     out->width = c->cfg.width;
@@ -333,7 +329,8 @@ int st_save(st_ctx *c, void *host_out, int64_t bytes) {
     o += row * c->cfg.width;
     ST_HIP(hipMemcpy2D(o, row, c->stats, pitch, row, ST_NSTAT, hipMemcpyDeviceToHost));
     o += row * ST_NSTAT;
-    ST_HIP(hipMemcpy(o, c->mt, row * st::kMtN, hipMemcpyDeviceToHost));
+    const size_t mrow = (size_t)st::kMtN * 4, mpitch = (size_t)st::kMtPitch * 4;
+    ST_HIP(hipMemcpy2D(o, mrow, c->mt, mpitch, mrow, (size_t)c->n, hipMemcpyDeviceToHost));
     return ST_OK;
 }
 
@@ -351,15 +348,22 @@ int st_load(st_ctx *c, const void *host_in, int64_t bytes) {
     if (h.width != c->cfg.width || h.height != c->cfg.height || h.n != c->n)
         return fail(ST_EINVAL, "st_load: snapshot of %lld %dx%d envs, context has %lld %dx%d",
                     (long long)h.n, h.width, h.height, (long long)c->n, c->cfg.width, c->cfg.height);
-    DeviceGuard g(c->device);
     const char *in = static_cast<const char *>(host_in) + sizeof(h);
     const size_t row = (size_t)c->n * 4, pitch = (size_t)c->stride * 4;
+    {  // MT indexes must be CPython's (0..624): st_save writes them synced
+        const int32_t *mi = reinterpret_cast<const int32_t *>(in + row * c->cfg.width) + ST_STAT_MT_INDEX * c->n;
+        for (int64_t e = 0; e < c->n; ++e)
+            if (mi[e] < 0 || mi[e] > st::kMtN)
+                return fail(ST_EINVAL, "st_load: env %lld has MT index %d outside [0, 624]", (long long)e, mi[e]);
+    }
+    DeviceGuard g(c->device);
     ST_HIP(hipDeviceSynchronize());
     ST_HIP(hipMemcpy2D(c->board, pitch, in, row, row, c->cfg.width, hipMemcpyHostToDevice));
     in += row * c->cfg.width;
     ST_HIP(hipMemcpy2D(c->stats, pitch, in, row, row, ST_NSTAT, hipMemcpyHostToDevice));
     in += row * ST_NSTAT;
-    ST_HIP(hipMemcpy(c->mt, in, row * st::kMtN, hipMemcpyHostToDevice));
+    const size_t mrow = (size_t)st::kMtN * 4, mpitch = (size_t)st::kMtPitch * 4;
+    ST_HIP(hipMemcpy2D(c->mt, mpitch, in, mrow, mrow, (size_t)c->n, hipMemcpyHostToDevice));
     ST_HIP(hipDeviceSynchronize());
     c->seeded = c->reset_once = true;
     return ST_OK;

@@ -223,137 +223,169 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
     return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
 }
 
-// ---- Incremental twist -------------------------------------------------------
-// CPython refills its 624 words all at once when the index reaches 624:
-//   mt[k] = X_k ^ mix(mt[k], mt[k+1]),  X_k = mt[k+397] (k < 227) | mt[k-227] (k >= 227),
-//   and mt[623] = mt[396] ^ mix(mt[623], mt[0]),
-// in place, in index order.  Evaluated in the same order one word at a time,
-// every operand is old exactly where CPython's is old (mt[k], mt[k+1],
-// mt[k+397]) and new where CPython's is new (mt[k-227], mt[396], mt[0]), so a
-// generation can be materialized lazily, as draws reach it: no wave ever runs
-// the 624-word twist (which made a twisting wave 2x slower than the others and
-// set the step's length whenever one occurred).
+// ---- Double-buffered twist --------------------------------------------------
+// CPython refills its 624 words at once when the index reaches 624:
+//   new[k] = X_k ^ mix(old[k], old[k+1]),  X_k = old[k+397] (k < 227) | new[k-227] (k >= 227),
+//   new[623] = new[396] ^ mix(old[623], new[0]).
+// Each env keeps two generation buffers A and B (kMtPitch words: A[624] B[624]
+// pad[4]).  Draws read the current one; the next generation is computed into
+// the other, one aligned 4-word block per locking step (mt_work), from the
+// current buffer and finished words of the next.  A draw uses 1/P(accept) <= 2
+// words on average, so a generation lasts >= ~312 draws and its successor is
+// ready after 156: the switch at index 624 is a bit flip, and no wave runs the
+// 624-word twist on the hot path (eagerly, a twisting wave took ~16k cycles,
+// 2x the others, and set the step's length whenever one occurred).  A
+// successor not ready in time (a host-written state restarts the progress at
+// 0) is finished wave-cooperatively (mt_finish).
 //
-// State encoding (stats row ST_STAT_MT_INDEX): idx | (M << 16).
-//   M = 0      : CPython's state -- every word of the current generation, idx =
-//                CPython's index (624: the next draw starts a generation).
-//   M = m + 1  : a generation in progress: words [0, m) new, [m, 624) of the
-//                previous generation, idx <= m.
-// st_mt_sync (k_mt_sync) completes pending generations before the host reads
-// the state; every writer of state from the host writes M = 0.
-__device__ __forceinline__ void mt_unpack(uint32_t r, int &idx, int &m) {
-    idx = (int)(r & 0xFFFFu);
-    m = (r >> 16) ? (int)(r >> 16) - 1 : kMtN;
+// Layout: cur[624] is next[0] for both parities -- B[0] for cur = A; the pad,
+// which the writer of A[0..3] also fills, for cur = B -- so a block's operands
+// cur[p..p+4] and cur[p+397..p+400] (p <= 224; X_227 = new[0]) need no case
+// split, and neither does new[623]'s mix(old[623], new[0]).
+//
+// State (stats row ST_STAT_MT_INDEX): idx | p << 10 | cur << 20
+//   idx: CPython's index into the current buffer (0..624)
+//   p  : words of the next generation done (multiple of 4, 0..624)
+//   cur: 0 = A, 1 = B.
+// A host-written CPython index (p = cur = 0, state in A) is always valid;
+// st_mt_sync (k_mt_sync) brings every env back to that form.
+constexpr uint32_t kMtB = kMtN;        // word offset of buffer B
+constexpr uint32_t kMtPad = 2 * kMtN;  // the pad: a copy of A[0..3]
+__device__ __forceinline__ void mt_unpack(uint32_t r, int &idx, int &pg, int &cur) {
+    idx = (int)(r & 0x3FFu);
+    pg = (int)((r >> 10) & 0x3FFu);
+    cur = (int)((r >> 20) & 1u);
 }
-__device__ __forceinline__ uint32_t mt_pack(int idx, int m) {
-    return (uint32_t)idx | (m < kMtN ? (uint32_t)(m + 1) << 16 : 0u);
-}
-// A complete generation that has been used up starts the next one (lazily).
-__device__ __forceinline__ void mt_begin(int &idx, int &m) {
-    if (idx >= kMtN && m >= kMtN) {
-        idx = 0;
-        m = 0;
-    }
+__device__ __forceinline__ uint32_t mt_pack(int idx, int pg, int cur) {
+    return (uint32_t)idx | ((uint32_t)pg << 10) | ((uint32_t)cur << 20);
 }
 
-// The 8 words a draw reads at index idx (idx < 624), and the operands that
-// materialize those not yet of the current generation.  a[0..8]: words
-// idx..idx+8 (a[j + 1] = mt[k+1]); bhi / blo: words idx+397.. / idx-227.. (X_k
-// for k < 227 / k >= 227, also mt[396] for k = 623); w0 = mt[0].  Buffer
-// loads through the wave's MT resource (mt_res): lanes or operands not wanted
-// get an out-of-range offset and read 0, so every load is issued on one path
-// (no branch, no merge of loaded and zero registers that would make the
-// compiler wait for the loads right here).  Reads past an env's state land in
-// a neighbour's state or the allocation's pads (values never used).
-struct MtWin {
-    uint32_t a[12], bhi[8], blo[8], w0;
-};
+// The wave's 64 MT states as one buffer resource.  Loads and stores of lanes
+// (or operands) not wanted get an out-of-range offset (loads read 0), so each
+// is issued on one path: no branch, and no merge of loaded and zeroed
+// registers, which would make the compiler wait for the loads on the spot.
 struct MtRes {
     __amdgpu_buffer_rsrc_t r;
-    uint32_t lane_off;  // byte offset of this lane's word 0
+    uint32_t lane_off;  // byte offset of this lane's buffer A
 };
 __device__ __forceinline__ MtRes mt_res(uint32_t *mt_wave, int lane) {
     MtRes m;
-    m.r = buf_rsrc(mt_wave - kMtPadFront, (uint32_t)((kWave * kMtN + kMtPadFront + kMtPadBack) * 4));
-    m.lane_off = (uint32_t)(lane * kMtN + kMtPadFront) * 4u;
+    m.r = buf_rsrc(mt_wave, (uint32_t)((kWave * kMtPitch + kMtPadBack) * 4));
+    m.lane_off = (uint32_t)(lane * kMtPitch) * 4u;
     return m;
 }
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ void mt_win_load(const MtRes &rs, int idx, int m, bool want, MtWin &w) {
-    const uint32_t base = rs.lane_off + 4u * (uint32_t)idx;
-#ifdef ST_AB_NOHI
-    const bool hi = false;
-#else
-    const bool hi = want && idx + 8 > m;  // the window reaches words of the previous generation
-#endif
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {  // cached loads (nt: packed rollout -12%)
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs.r, want ? base + 16u * q : kOff, 0, 0);
-        w.a[4 * q] = v.x, w.a[4 * q + 1] = v.y, w.a[4 * q + 2] = v.z, w.a[4 * q + 3] = v.w;
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const u32x4 h = __builtin_amdgcn_raw_buffer_load_b128(rs.r, hi ? base + 4u * 397u + 16u * q : kOff, 0, 0);
-        const u32x4 l = __builtin_amdgcn_raw_buffer_load_b128(rs.r, hi ? base - 4u * 227u + 16u * q : kOff, 0, 0);
-        w.bhi[4 * q] = h.x, w.bhi[4 * q + 1] = h.y, w.bhi[4 * q + 2] = h.z, w.bhi[4 * q + 3] = h.w;
-        w.blo[4 * q] = l.x, w.blo[4 * q + 1] = l.y, w.blo[4 * q + 2] = l.z, w.blo[4 * q + 3] = l.w;
-    }
-    w.w0 = __builtin_amdgcn_raw_buffer_load_b32(rs.r, hi ? rs.lane_off : kOff, 0, 0);
+__device__ __forceinline__ u32x4 mt_ld16(const MtRes &rs, bool on, uint32_t word) {
+    return __builtin_amdgcn_raw_buffer_load_b128(rs.r, on ? rs.lane_off + 4u * word : kOff, 0, 0);
 }
 
-// Take all window words now (one vmcnt(#younger ops) wait on a single path):
-// words never read would otherwise stay "pending" for the compiler, and every
-// later reuse of their registers would wait vmcnt(0), draining the step's
-// early stores.
-__device__ __forceinline__ void mt_win_consume(const MtWin &w) {
-    asm volatile("" ::"v"(w.a[0]), "v"(w.a[1]), "v"(w.a[2]), "v"(w.a[3]), "v"(w.a[4]), "v"(w.a[5]),
-                 "v"(w.a[6]), "v"(w.a[7]), "v"(w.a[8]), "v"(w.a[9]), "v"(w.a[10]), "v"(w.a[11]));
-    asm volatile("" ::"v"(w.bhi[0]), "v"(w.bhi[1]), "v"(w.bhi[2]), "v"(w.bhi[3]), "v"(w.bhi[4]),
-                 "v"(w.bhi[5]), "v"(w.bhi[6]), "v"(w.bhi[7]), "v"(w.w0));
-    asm volatile("" ::"v"(w.blo[0]), "v"(w.blo[1]), "v"(w.blo[2]), "v"(w.blo[3]), "v"(w.blo[4]),
-                 "v"(w.blo[5]), "v"(w.blo[6]), "v"(w.blo[7]));
+// Loaded for a locking lane before its lock path (consumed after it): the
+// draw window cur[idx..idx+7] and the operands of the next block.  Reads past
+// an env's state land in the next env's state or the allocation's back pad.
+struct MtPre {
+    uint32_t w[8], a[5], x[4];
+};
+__device__ __forceinline__ void mt_pre_load(const MtRes &rs, uint32_t mtst, bool want, MtPre &q) {
+    int idx, pg, cur;
+    mt_unpack(mtst, idx, pg, cur);
+    const uint32_t cb = cur ? kMtB : 0u, nb = cur ? 0u : kMtB;
+    const bool work = want && pg < kMtN;
+    const u32x4 w0 = mt_ld16(rs, want, cb + idx), w1 = mt_ld16(rs, want, cb + idx + 4);
+    const u32x4 a = mt_ld16(rs, work, cb + pg);
+    const u32x4 x = mt_ld16(rs, work, pg <= 224 ? cb + pg + 397 : nb + pg - 227);
+    q.a[4] = __builtin_amdgcn_raw_buffer_load_b32(rs.r, work ? rs.lane_off + 4u * (cb + pg + 4) : kOff, 0, 0);
+    q.w[0] = w0.x, q.w[1] = w0.y, q.w[2] = w0.z, q.w[3] = w0.w;
+    q.w[4] = w1.x, q.w[5] = w1.y, q.w[6] = w1.z, q.w[7] = w1.w;
+    q.a[0] = a.x, q.a[1] = a.y, q.a[2] = a.z, q.a[3] = a.w;
+    q.x[0] = x.x, q.x[1] = x.y, q.x[2] = x.z, q.x[3] = x.w;
+}
+// Take all prefetched words at once (one vmcnt wait on a single path): words
+// never read would stay "pending" for the compiler, and every later reuse of
+// their registers would wait vmcnt(0), draining the step's early stores.
+__device__ __forceinline__ void mt_pre_consume(const MtPre &q) {
+    asm volatile("" ::"v"(q.w[0]), "v"(q.w[1]), "v"(q.w[2]), "v"(q.w[3]), "v"(q.w[4]), "v"(q.w[5]),
+                 "v"(q.w[6]), "v"(q.w[7]));
+    asm volatile("" ::"v"(q.a[0]), "v"(q.a[1]), "v"(q.a[2]), "v"(q.a[3]), "v"(q.a[4]), "v"(q.x[0]),
+                 "v"(q.x[1]), "v"(q.x[2]), "v"(q.x[3]));
 }
 
-// The window's words of the current generation (word[j] = mt[idx + j]); those
-// at or past m are materialized and written back (buffer stores: masked-off
-// words go out of range), and m advances past the window.  Branch-free: the
-// recurrence is evaluated for all 8 words and masked in.
-__device__ __forceinline__ void mt_win_resolve(const MtRes &rs, int idx, int &m, bool want,
-                                               const MtWin &w, uint32_t (&word)[8]) {
+// One block of the next generation, next[p..p+3] (lanes with `want` and
+// p < 624), as one 16-B store (+ the pad copy for next = A, p = 0).
+__device__ __forceinline__ void mt_work(const MtRes &rs, bool want, uint32_t &mtst, const MtPre &q) {
+    int idx, pg, cur;
+    mt_unpack(mtst, idx, pg, cur);
+    const bool work = want && pg < kMtN;
+    uint4 v;
+    v.x = q.x[0] ^ mt_mix(q.a[0], q.a[1]);
+    v.y = q.x[1] ^ mt_mix(q.a[1], q.a[2]);
+    v.z = q.x[2] ^ mt_mix(q.a[2], q.a[3]);
+    v.w = q.x[3] ^ mt_mix(q.a[3], q.a[4]);
+    const uint32_t nb = cur ? 0u : kMtB;
+    buf_store16(rs.r, work ? rs.lane_off + 4u * (nb + (uint32_t)pg) : kOff, v);
+    buf_store16(rs.r, work && cur && pg == 0 ? rs.lane_off + 4u * kMtPad : kOff, v);
+    if (work) mtst = mt_pack(idx, pg + 4, cur);
+}
+
+// Finish the next generation of ONE env (words [pg, 624)), wave-cooperatively
+// (wave-uniform arguments): the chunked recurrence in LDS -- [0,227) reads old
+// words | [227,454) reads [0,227) | [454,623) reads [227,396) | 623 reads 396
+// and 0, each chunk only words that are old or finished.
+__device__ void mt_finish(uint32_t *g, uint32_t *S, int lane, int pg, int cur) {
+    const uint32_t *src_new = g + (cur ? 0 : kMtB), *src_old = g + (cur ? kMtB : 0);
+    uint32_t *dst = g + (cur ? 0 : kMtB);
+    {
+        uint32_t t[10];  // 624 = 9 * 64 + 48: issue all ten loads before any wait
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int k = idx + j;
-        const uint32_t x = k < 227 ? w.bhi[j] : w.blo[j];
-        const uint32_t b = k == kMtN - 1 ? w.w0 : w.a[j + 1];
-        const uint32_t f = 0u - (uint32_t)(k >= m);
-#ifdef ST_AB_NOMIX
-        word[j] = w.a[j] ^ (x & f);
-#else
-        word[j] = w.a[j] ^ ((x ^ mt_mix(w.a[j], b) ^ w.a[j]) & f);
-#endif
-#ifdef ST_AB_NOSTORE
-        const bool st = false;
-#else
-        const bool st = want && k >= m && k < kMtN;
-#endif
-        __builtin_amdgcn_raw_buffer_store_b32(word[j], rs.r, st ? rs.lane_off + 4u * (uint32_t)k : kOff, 0, 0);
+        for (int q = 0; q < 10; ++q) {
+            const int i = lane + kWave * q;
+            t[q] = i < kMtN ? (i < pg ? src_new[i] : src_old[i]) : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 10; ++q) {
+            const int i = lane + kWave * q;
+            if (i < kMtN) S[i] = t[q];
+        }
     }
-    if (want && idx + 8 > m) m = idx + 8 < kMtN ? idx + 8 : kMtN;
+    wave_sync();
+    uint32_t v[4];
+    auto chunk = [&](int lo, int hi, int xoff) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = lo + lane + kWave * q;
+            if (k < hi && k >= pg) v[q] = S[k + xoff] ^ mt_mix(S[k], S[k + 1]);
+        }
+        wave_sync();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = lo + lane + kWave * q;
+            if (k < hi && k >= pg) S[k] = v[q];
+        }
+        wave_sync();
+    };
+    chunk(0, 227, 397);
+    chunk(227, 454, -227);
+    chunk(454, 623, -227);
+    if (lane == 0 && pg <= 623) S[623] = S[396] ^ mt_mix(S[623], S[0]);
+    wave_sync();
+    for (int i = lane; i < kMtN; i += kWave)
+        if (i >= pg) dst[i] = S[i];
+    if (cur && lane < 4) g[kMtPad + lane] = S[lane];
+    __builtin_amdgcn_s_waitcnt(0);  // rare path: stores done before the wave reads them back
+    wave_sync();
 }
 
 // _choose_shape (tetris_env.py:183-191) + the count update of _new_piece
 // (:199) for every lane with `need`: randint(1, sum(m)) = 1 + _randbelow(n)
 // with rejection sampling on getrandbits(k) (Lib/random.py:239-249).  `mtst`
-// is the lane's packed MT index (see mt_pack).  Wave-uniform: every lane of
-// the wave calls it.  `pre`: the window the caller loaded for lanes with
-// `have_pre` (at the index mt_begin gives).  The common case is branch-free:
-// all 8 words tempered as independent chains, each lane takes its first
-// accepted one; lanes the window does not settle (8 rejections, p <= 2^-8)
-// load the next window in the loop.
+// is the lane's packed MT state (mt_pack).  Wave-uniform: every lane of the
+// wave calls it.  `pre`: the window the caller loaded for lanes with
+// `have_pre`.  The common case is branch-free: all 8 words tempered as
+// independent chains, each lane takes its first accepted one; lanes the
+// window does not settle (8 rejections, p <= 2^-8, or the generation's end)
+// continue in the loop, switching generations at index 624.
 __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t &mtst,
-                                          uint32_t *mt_wave, int lane, const MtWin &pre,
-                                          bool have_pre) {
+                                          uint32_t *mt_wave, uint32_t *S, int lane,
+                                          const MtPre &pre, bool have_pre) {
     int32_t maxc = cnt[0], sumc = cnt[0];
 #pragma unroll
     for (int i = 1; i < 7; ++i) {
@@ -362,21 +394,17 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
     }
     const uint32_t n = (uint32_t)(35 + 7 * maxc - sumc);
     const int kb = 32 - __builtin_clz(n);
-    const MtRes rs = mt_res(mt_wave, lane);
-    int idx, m;
-    mt_unpack(mtst, idx, m);
-    if (need) mt_begin(idx, m);
+    int idx, pg, cur;
+    mt_unpack(mtst, idx, pg, cur);
     bool pending = need;
     uint32_t r = 0;
-    mt_win_consume(pre);
-    uint32_t word[8];
+    mt_pre_consume(pre);
     if (have_pre && pending) {
-        mt_win_resolve(rs, idx, m, true, pre, word);
         int first = 8;
         uint32_t rr = 0;
 #pragma unroll
         for (int j = 7; j >= 0; --j) {
-            const uint32_t y = mt_temper(word[j]) >> (32 - kb);
+            const uint32_t y = mt_temper(pre.w[j]) >> (32 - kb);
             const bool acc = y < n && idx + j < kMtN;
             first = acc ? j : first;
             rr = acc ? y : rr;
@@ -389,26 +417,41 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
             idx = idx + 8 < kMtN ? idx + 8 : kMtN;
         }
     }
-    while (__ballot(pending)) {
-        if (pending) mt_begin(idx, m);
-        MtWin w;
-        mt_win_load(rs, idx, m, pending, w);
-        mt_win_consume(w);
-        mt_win_resolve(rs, idx, m, pending, w, word);
+    if (__ballot(pending)) {
+        const MtRes rs = mt_res(mt_wave, lane);
+        do {
+            // lanes at the end of their generation switch to the next one,
+            // finishing it first where mt_work has not
+            const bool sw = pending && idx >= kMtN;
+            uint64_t fin = __ballot(sw && pg < kMtN);
+            while (fin) {
+                const int l = __builtin_ctzll(fin);
+                fin &= fin - 1;
+                mt_finish(mt_wave + (size_t)l * kMtPitch, S, lane, __shfl(pg, l), __shfl(cur, l));
+            }
+            if (sw) {
+                cur ^= 1;
+                idx = 0;
+                pg = 0;
+            }
+            const uint32_t cb = cur ? kMtB : 0u;
+            const u32x4 w0 = mt_ld16(rs, pending, cb + idx), w1 = mt_ld16(rs, pending, cb + idx + 4);
+            const uint32_t word[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            if (!__ballot(pending && idx < kMtN)) break;
-            if (pending && idx < kMtN) {
-                const uint32_t y = mt_temper(word[j]) >> (32 - kb);
-                ++idx;
-                if (y < n) {
-                    pending = false;
-                    r = y;
+            for (int j = 0; j < 8; ++j) {
+                if (!__ballot(pending && idx < kMtN)) break;
+                if (pending && idx < kMtN) {
+                    const uint32_t y = mt_temper(word[j]) >> (32 - kb);
+                    ++idx;
+                    if (y < n) {
+                        pending = false;
+                        r = y;
+                    }
                 }
             }
-        }
+        } while (__ballot(pending));
     }
-    if (need) mtst = mt_pack(idx, m);
+    if (need) mtst = mt_pack(idx, pg, cur);
     if (!need) return 0;
     int32_t rr = (int32_t)r + 1;
     int pick = 6;
@@ -424,50 +467,6 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
 #pragma unroll
     for (int i = 0; i < 7; ++i) cnt[i] += (i == pick);
     return pick;
-}
-
-// Complete a pending generation of ONE env (st_mt_sync): words [m, 624) by
-// the chunked recurrence, wave-cooperatively (all 64 lanes, wave-uniform m):
-// [0,227) reads old words | [227,454) reads [0,227) | [454,623) reads
-// [227,396) | 623 reads 396 and 0 -- each chunk only reads words that are
-// old or finished.
-__device__ void coop_complete(uint32_t *g, uint32_t *S, int lane, int m) {
-    {
-        uint32_t t[10];  // 624 = 9 * 64 + 48: issue all ten loads before any wait
-#pragma unroll
-        for (int q = 0; q < 10; ++q) {
-            const int i = lane + kWave * q;
-            t[q] = i < kMtN ? g[i] : 0u;
-        }
-#pragma unroll
-        for (int q = 0; q < 10; ++q) {
-            const int i = lane + kWave * q;
-            if (i < kMtN) S[i] = t[q];
-        }
-    }
-    wave_sync();
-    uint32_t v[4];
-    auto chunk = [&](int lo, int hi, int xoff) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int k = lo + lane + kWave * q;
-            if (k < hi && k >= m) v[q] = S[k + xoff] ^ mt_mix(S[k], S[k + 1]);
-        }
-        wave_sync();
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int k = lo + lane + kWave * q;
-            if (k < hi && k >= m) S[k] = v[q];
-        }
-        wave_sync();
-    };
-    chunk(0, 227, 397);
-    chunk(227, 454, -227);
-    chunk(454, 623, -227);
-    if (lane == 0 && m <= 623) S[623] = S[396] ^ mt_mix(S[623], S[0]);
-    wave_sync();
-    for (int i = lane; i < kMtN; i += kWave)
-        if (i >= m) g[i] = S[i];
 }
 
 __device__ __forceinline__ uint32_t pack_piece(int id, int rot, int ax, int ay, int lock) {
@@ -499,11 +498,12 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     if constexpr (STAMP) rt0 = __builtin_amdgcn_s_memrealtime();
     ST_STAMP(0);
     // LDS: board columns L[x + kPad][lane] (walls at both ends), the staged
-    // counter rows SS[r][lane] (r < 14: stats rows, 14: piece word) and the
-    // piece table.
+    // counter rows SS[r][lane] (r < 14: stats rows, 14: piece word), the
+    // piece table and the MT scratch of mt_finish.
     __shared__ __attribute__((aligned(16))) uint32_t L[(kMaxW + 2 * kPad) * kWave];
     __shared__ __attribute__((aligned(16))) uint32_t SS[kHotQ * 4 * kWave];
     __shared__ uint2 T2[28];
+    __shared__ uint32_t S[kMtN];
     // st_step: per env board keep-mask, changed board columns, changed counter rows
     __shared__ __attribute__((aligned(16))) uint32_t KM[KSTEPS == 1 ? kWave : 4];
     __shared__ __attribute__((aligned(16))) uint32_t BD[KSTEPS == 1 ? kWave : 4];
@@ -655,16 +655,12 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     ST_STAMP(2);
     // MT window for the piece this lock will draw: issued now, consumed after
     // the lock path (every locking lane draws: a spawn, or the same-step
-    // reset's).  mt_begin only positions the window; the draw commits.
+    // reset's), and the operands of its next-generation block (mt_work).
     uint32_t mtst = ss(ST_STAT_MT_INDEX);  // packed (mt_pack)
     const bool want_pre = locknow && !(p.ablate & 2u);
-    MtWin pre;
-    {
-        int pidx, pm;
-        mt_unpack(mtst, pidx, pm);
-        mt_begin(pidx, pm);
-        mt_win_load(mt_res(p.mt + e0 * kMtN, lane), pidx, pm, want_pre, pre);
-    }
+    const MtRes mrs = mt_res(p.mt + e0 * kMtPitch, lane);
+    MtPre pre;
+    mt_pre_load(mrs, mtst, want_pre, pre);
 
     // ---- lock path (tetris_env.py:263-299) ----
     bool died = false, spawn = false;
@@ -813,10 +809,14 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         ST_STAMP(9);
     }
-    if (!(p.ablate & 2u)) pick = draw_shape(draw, cnt, mtst, p.mt + e0 * kMtN, lane, pre, want_pre);
+    if (!(p.ablate & 2u)) {
+        mt_pre_consume(pre);
+        mt_work(mrs, want_pre, mtst, pre);  // before the draw: a switch it makes resets the progress
+        pick = draw_shape(draw, cnt, mtst, p.mt + e0 * kMtPitch, S, lane, pre, want_pre);
+    }
     ST_STAMP(4);
     if constexpr (STAMP) {  // 1: a draw started a generation, 2: a draw ran past its 8 words
-        const int i0 = (int)(mt_before & 0xFFFFu), i1 = (int)(mtst & 0xFFFFu);
+        const int i0 = (int)(mt_before & 0x3FFu), i1 = (int)(mtst & 0x3FFu);
         draw_kind = (__ballot(draw && i1 < i0) ? 1u : 0u) | (__ballot(draw && i1 >= i0 && i1 - i0 > 8) ? 2u : 0u);
     }
     uint2 odesc = desc;
@@ -905,7 +905,17 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
                 const int cr = c - ee * CPE;
                 const int x = cr / CPC;
                 const int q = cr - x * CPC;
-                out4[c] = F4[(O[ee * (WT + 1) + x] >> (4 * q)) & 15u];
+                const float4 f = F4[(O[ee * (WT + 1) + x] >> (4 * q)) & 15u];
+                if constexpr (KSTEPS != 1) {
+                    // rollouts: non-temporal (A/B: -13% f32 rollout; the MT and
+                    // state lines stay in L2 instead of the streamed obs; +7% on
+                    // the single-step launch, so not there)
+                    typedef float f32x4 __attribute__((ext_vector_type(4)));
+                    const f32x4 fv = {f.x, f.y, f.z, f.w};
+                    __builtin_nontemporal_store(fv, reinterpret_cast<f32x4 *>(&out4[c]));
+                } else {
+                    out4[c] = f;
+                }
             }
         } else {
             const int per_env = W * H;
@@ -994,6 +1004,7 @@ __global__ __launch_bounds__(kWave) void k_rollout(KParams p) {
 // TetrisEngine.clear (tetris_env.py:306-315) on masked envs.  n_deaths,
 // shape_counts and the lock-delay counter persist (R15).
 __global__ __launch_bounds__(kWave) void k_reset(KParams p) {
+    __shared__ uint32_t S[kMtN];
     const int lane = threadIdx.x;
     const int64_t e0 = (int64_t)blockIdx.x * kWave;
     const int64_t e = e0 + lane;
@@ -1005,8 +1016,8 @@ __global__ __launch_bounds__(kWave) void k_reset(KParams p) {
     for (int i = 0; i < 7; ++i) cnt[i] = st[(ST_STAT_COUNT0 + i) * sd];
     uint32_t mtst = (uint32_t)st[ST_STAT_MT_INDEX * sd];
     const uint32_t pw = p.piece[e];
-    const MtWin nopre{};
-    const int pick = draw_shape(m, cnt, mtst, p.mt + e0 * kMtN, lane, nopre, false);
+    const MtPre nopre{};
+    const int pick = draw_shape(m, cnt, mtst, p.mt + e0 * kMtPitch, S, lane, nopre, false);
     if (m) {
         st[ST_STAT_TIME * sd] = 0;
         st[ST_STAT_SCORE * sd] = 0;
@@ -1031,7 +1042,7 @@ __global__ void k_seed(KParams p) {
     const uint64_t s = p.seeds[e];
     const uint32_t key[2] = {(uint32_t)s, (uint32_t)(s >> 32)};
     const int len = (s >> 32) ? 2 : 1;
-    uint32_t *g = p.mt + e * kMtN;
+    uint32_t *g = p.mt + e * kMtPitch;  // buffer A
     uint32_t prev = 19650218u;  // init_genrand(19650218)
     g[0] = prev;
     for (int i = 1; i < kMtN; ++i) {
@@ -1080,25 +1091,34 @@ __global__ void k_seed(KParams p) {
 }
 
 // ---------------------------------------------------------------- MT sync
-// st_mt_sync: finish every generation the draws left in progress (M != 0), so
-// that stats/mt hold CPython's state again.  One wave per 64 envs; the wave
-// completes its pending lanes' states one after another, cooperatively.
+// st_mt_sync: every env back to CPython's form (see "Double-buffered twist"):
+// where the current generation is in B, B is copied to A; the index loses the
+// engine bits (the next generation's progress restarts at 0).  One wave per
+// 64 envs; it copies its lanes' B buffers one env at a time, cooperatively.
 __global__ __launch_bounds__(kWave) void k_mt_sync(KParams p) {
-    __shared__ uint32_t S[kMtN];
     const int lane = threadIdx.x;
     const int64_t e0 = (int64_t)blockIdx.x * kWave;
     const int64_t e = e0 + lane;
     int32_t *row = p.stats + (int64_t)ST_STAT_MT_INDEX * p.stride;
     const uint32_t r = (uint32_t)row[e];
-    uint64_t pend = __ballot((r >> 16) != 0u);
-    while (pend) {
-        const int l = __builtin_ctzll(pend);
-        pend &= pend - 1;
-        const uint32_t rl = __shfl(r, l);
-        coop_complete(p.mt + (e0 + l) * kMtN, S, lane, (int)(rl >> 16) - 1);
-        wave_sync();
+    uint64_t inb = __ballot((r >> 20) & 1u);
+    while (inb) {
+        const int l = __builtin_ctzll(inb);
+        inb &= inb - 1;
+        uint32_t *g = p.mt + (e0 + l) * kMtPitch;
+        uint32_t t[10];
+#pragma unroll
+        for (int q = 0; q < 10; ++q) {
+            const int i = lane + kWave * q;
+            t[q] = i < kMtN ? g[kMtB + i] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 10; ++q) {
+            const int i = lane + kWave * q;
+            if (i < kMtN) g[i] = t[q];
+        }
     }
-    if ((r >> 16) != 0u) row[e] = (int32_t)(r & 0xFFFFu);
+    if ((r >> 10) != 0u) row[e] = (int32_t)(r & 0x3FFu);
 }
 
 // ---------------------------------------------------------------- render

@@ -58,7 +58,8 @@ class StateViews(ctypes.Structure):
     _fields_ = [("board", ctypes.c_void_p), ("piece", ctypes.c_void_p),
                 ("stats", ctypes.c_void_p), ("mt", ctypes.c_void_p),
                 ("n_envs", ctypes.c_int64), ("stride", ctypes.c_int64),
-                ("width", ctypes.c_int32), ("height", ctypes.c_int32)]
+                ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("mt_pitch", ctypes.c_int64)]
 
 
 _lib = None

@@ -211,7 +211,7 @@ class TetrisBatch:
     # ------------------------------------------------------------ state
     def _sizes(self):
         W, sd = self.width, self.stride
-        return dict(board=(W, sd), piece=(sd,), stats=(C.NSTAT, sd), mt=(sd, C.MT_N))
+        return dict(board=(W, sd), piece=(sd,), stats=(C.NSTAT, sd), mt=(sd, int(self._views.mt_pitch)))
 
     def _view_ptr(self, name):
         return getattr(self._views, name)
@@ -224,10 +224,12 @@ class TetrisBatch:
         with torch.cuda.device(self.device):
             C.check(self._L.st_mt_sync(self._ctx, self._stream()))
 
-    def state_tensors(self, fields=("board", "piece", "stats")) -> dict:
-        """Device copies of the state (full stride; slice [..., :n] for real envs)."""
+    def state_tensors(self, fields=("board", "piece", "stats"), sync: bool = True) -> dict:
+        """Device copies of the state (full stride; slice [..., :n] for real envs).
+        `sync=False` skips st_mt_sync: the MT index row then carries engine
+        bits (the counters are exact either way)."""
         out = {}
-        if "stats" in fields or "mt" in fields:
+        if sync and ("stats" in fields or "mt" in fields):
             self.sync_mt()
         with torch.cuda.device(self.device):
             for f in fields:
@@ -247,7 +249,7 @@ class TetrisBatch:
             a = v.cpu().numpy()
             if f in ("board", "piece", "mt"):
                 a = a.view(np.uint32)
-            out[f] = a[: self.n] if f == "mt" else a[..., : self.n]
+            out[f] = a[: self.n, : C.MT_N] if f == "mt" else a[..., : self.n]
         return out
 
     def set_state(self, **fields):
@@ -262,7 +264,7 @@ class TetrisBatch:
                 full = cur[f].cpu().numpy().view(np.uint32).copy()
                 v = np.asarray(v).astype(np.int64).astype(np.uint32)
                 if f == "mt":
-                    full[: self.n] = v
+                    full[: self.n, : C.MT_N] = v
                 else:
                     full[..., : self.n] = v
                 t = torch.from_numpy(full.view(np.int32)).to(self.device)
@@ -304,7 +306,7 @@ class TetrisBatch:
 
     def info_tensors(self) -> dict:
         """get_info() (tetris_env.py:232-241) for every env as int32 device tensors."""
-        st = self.state_tensors(("stats",))["stats"][:, : self.n]
+        st = self.state_tensors(("stats",), sync=False)["stats"][:, : self.n]
         return dict(time=st[C.STAT["time"]], score=st[C.STAT["score"]],
                     lines_cleared=st[C.STAT["lines"]], holes=st[C.STAT["holes"]],
                     deaths=st[C.STAT["deaths"]], piece_height=st[C.STAT["piece_height"]],

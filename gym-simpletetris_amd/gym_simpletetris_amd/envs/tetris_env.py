@@ -121,7 +121,8 @@ class TetrisEnv:
         v = self.engine._views
         L = self.engine._L
         s = self._stream()
-        self.engine.sync_mt()
+        if self._rng_mode == "global":  # CPython's random mirrors the env's MT state
+            self.engine.sync_mt()
         C.check(L.st_copy(ctypes.c_void_p(self._h_stats.ctypes.data), ctypes.c_void_p(v.stats),
                           self._h_stats.nbytes, s))
         torch.cuda.current_stream(self.engine.device).synchronize()

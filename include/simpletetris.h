@@ -104,7 +104,9 @@ enum st_stat {
  *            id in shape_names order T,J,L,Z,S,I,O (tetris_env.py:19);
  *            rot = number of rotate_left (rotated(cclk=False)) mod 4
  *   stats  : int32 [ST_NSTAT][stride]
- *   mt     : uint32 [stride][624] MT19937 words per env                      */
+ *   mt     : uint32 [stride][mt_pitch]; words [0, 624) of each row are the
+ *            env's MT19937 state (CPython random.getstate()) after st_mt_sync;
+ *            the rest is engine-private (the next generation, see st_mt_sync) */
 typedef struct st_state_views {
     uint32_t *board;
     uint32_t *piece;
@@ -113,6 +115,7 @@ typedef struct st_state_views {
     int64_t n_envs;
     int64_t stride;
     int32_t width, height;
+    int64_t mt_pitch; /* words between consecutive envs' rows of mt */
 } st_state_views;
 
 /* ---- lifecycle: TetrisEnv.__init__ (tetris_env.py:343-392) ---------------- */
@@ -181,14 +184,15 @@ int st_state(st_ctx *ctx, st_state_views *out);
  * between the views above and caller buffers (crafted states). */
 int st_copy(void *dst, const void *src, int64_t bytes, st_stream stream);
 
-/* The step kernels twist each env's MT19937 state lazily: a draw computes
- * only the words it reads, so between steps an env may hold a generation in
- * progress, marked in ST_STAT_MT_INDEX (index | (m + 1) << 16: words [0, m)
- * of the new generation, the rest of the old).  st_mt_sync completes those
- * generations on `stream`, after which every env's mt words and index are
- * exactly CPython's random.getstate() (index 0..624).  Call it before reading
- * stats or mt through st_state's views; st_save calls it itself.  Writing a
- * CPython state (index 0..624, no high bits) is always valid. */
+/* The step kernels keep each env's MT19937 generation double-buffered: the
+ * next generation is computed a few words per draw into a second buffer and
+ * becomes current at index 624, so between steps ST_STAT_MT_INDEX carries
+ * engine bits above bit 9 and the current words may sit in the second buffer.
+ * st_mt_sync (on `stream`) brings every env back to CPython's form: words
+ * [0, 624) of its mt row and an index 0..624 equal random.getstate().  Call it
+ * before reading stats or mt through st_state's views; st_save calls it
+ * itself.  Writing a CPython state (words [0, 624), index 0..624) is always
+ * valid. */
 int st_mt_sync(st_ctx *ctx, st_stream stream);
 
 /* State snapshot: the engine attributes of every env (board, piece, counters,

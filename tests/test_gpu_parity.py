@@ -410,11 +410,12 @@ def test_long_rejection_runs_and_twists(mode):
         assert np.array_equal(fin["mt"][i], np.ctypeslib.as_array(ob.envs[i].rng.mt)), i
 
 
-def test_lazy_twist_across_generations():
-    """Lock every step for ~2.5 MT generations: the in-kernel twist is lazy
-    (a draw materializes only its words), so states between steps hold
-    generations in progress; st_mt_sync must restore CPython's exact state at
-    any point, and syncing mid-run must not change what follows."""
+def test_mt_generations_across_steps():
+    """Lock every step for ~2.5 MT generations: the next generation is built
+    a block per draw into a second buffer and switched to at index 624, so
+    states between steps carry engine bits; st_mt_sync must restore CPython's
+    exact state at any point, and syncing mid-run (which restarts the next
+    generation's progress) must not change what follows."""
     import ctypes
     from gym_simpletetris_amd import _lib as C
     G = _engine()
@@ -445,7 +446,7 @@ def test_lazy_twist_across_generations():
         C.check(b._L.st_copy(ctypes.c_void_p(raw.data_ptr()),
                              ctypes.c_void_p(v.stats + C.STAT["mt_index"] * v.stride * 4),
                              raw.numel() * 4, b._stream()))
-        saw_lazy |= bool(((raw[:n].cpu().numpy() >> 16) != 0).any())
+        saw_lazy |= bool(((raw[:n].cpu().numpy() >> 20) != 0).any())   # current generation in B
         if (c0 // chunk) % 3 == 1:
             a.get_state(("mt", "stats"))                # sync a only, mid-run
     assert saw_lazy
