@@ -53,22 +53,23 @@ def algorithmic_bytes(width: int, height: int, p_lock: float, f32: bool) -> floa
     time 4 + reward 4 + done 1 + packed obs 4W (+ float32 obs 4WH).
     Per lock: counters (score, lines, holes, piece_height, deaths, 7 counts,
     MT index) read + written 2*13*4, board write 4W, MT words read 8, and the
-    amortised MT twist (2 x 2,496 B per 476 draws) 10.5."""
+    amortised next MT generation (2 x 2,496 B read + 2,496 B written per
+    ~476 draws) 15.7."""
     always = (1 + 4 + 4 + 4 * width) + (4 + 4 + 4 + 1 + 4 * width)
     if f32:
         always += 4 * width * height
-    lock = 2 * 13 * 4 + 4 * width + 8 + 10.5
+    lock = 2 * 13 * 4 + 4 * width + 8 + 15.7
     return always + lock * p_lock
 
 
 def rollout_bytes(width: int, height: int, p_lock: float, f32: bool, k: int) -> float:
     """Algorithmic HBM bytes per env-step of the K-step rollout kernel: per
     step read action 1, write packed obs 4W + reward 4 + done 1 (+ float32
-    obs 4WH); per lock MT words 8 + amortised twist 10.5; per launch the state
+    obs 4WH); per lock MT words 8 + amortised next generation 15.7; per launch the state
     (board 4W + 14 counters + piece) read and written once, / K."""
     step = 1 + 4 * width + 4 + 1 + (4 * width * height if f32 else 0)
     state = 2 * (4 * width + 15 * 4)
-    return step + 18.5 * p_lock + state / k
+    return step + 23.7 * p_lock + state / k
 
 
 def cpu_baseline(seconds: float, cfg_kw: dict):
