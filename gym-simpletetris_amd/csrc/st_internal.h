@@ -12,10 +12,10 @@ constexpr int kPad = 4;        // wall columns on each side of the LDS board
 constexpr int kMaxW = 32;
 constexpr int kMaxH = 28;
 constexpr int kMtN = 624;
-// Per-env MT storage (words): generation buffers A and B, then a 4-word pad
+// Per-env MT storage (words): generation buffers A and B, then a 16-word pad
 // (see st_kernels.hip, "Double-buffered twist"); 16-B aligned.
-constexpr int64_t kMtPitch = 2 * kMtN + 4;
-// after the last env: a draw window reads up to 8 words past index 623 of B
+constexpr int64_t kMtPitch = 2 * kMtN + 16;
+// after the last env: a draw window reads up to 16 words past index 623 of B
 constexpr int64_t kMtPadBack = 64;
 // diagnostic stamps per wave: 10 s_memtime phase stamps, s_memrealtime at
 // start and end, HW_ID, XCC_ID (16 words)

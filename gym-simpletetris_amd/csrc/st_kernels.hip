@@ -228,7 +228,7 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
 //   new[k] = X_k ^ mix(old[k], old[k+1]),  X_k = old[k+397] (k < 227) | new[k-227] (k >= 227),
 //   new[623] = new[396] ^ mix(old[623], new[0]).
 // Each env keeps two generation buffers A and B (kMtPitch words: A[624] B[624]
-// pad[4]).  Draws read the current one; the next generation is computed into
+// pad[16]).  Draws read the current one; the next generation is computed into
 // the other, one aligned 4-word block per locking step (mt_work), from the
 // current buffer and finished words of the next.  A draw uses 1/P(accept) <= 2
 // words on average, so a generation lasts >= ~312 draws and its successor is
@@ -238,10 +238,11 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
 // successor not ready in time (a host-written state restarts the progress at
 // 0) is finished wave-cooperatively (mt_finish).
 //
-// Layout: cur[624] is next[0] for both parities -- B[0] for cur = A; the pad,
-// which the writer of A[0..3] also fills, for cur = B -- so a block's operands
-// cur[p..p+4] and cur[p+397..p+400] (p <= 224; X_227 = new[0]) need no case
-// split, and neither does new[623]'s mix(old[623], new[0]).
+// Layout: cur[624..639] is next[0..15] for both parities -- B[0..15] for cur
+// = A; the pad, which the writers of A[0..15] also fill, for cur = B -- so a
+// block's operands cur[p..p+4] and cur[p+397..p+400] (p <= 224; X_227 =
+// new[0]) need no case split, neither does new[623]'s mix(old[623], new[0]),
+// and a draw window that runs past 623 continues into a complete successor.
 //
 // State (stats row ST_STAT_MT_INDEX): idx | p << 10 | cur << 20
 //   idx: CPython's index into the current buffer (0..624)
@@ -250,7 +251,8 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
 // A host-written CPython index (p = cur = 0, state in A) is always valid;
 // st_mt_sync (k_mt_sync) brings every env back to that form.
 constexpr uint32_t kMtB = kMtN;        // word offset of buffer B
-constexpr uint32_t kMtPad = 2 * kMtN;  // the pad: a copy of A[0..3]
+constexpr uint32_t kMtPad = 2 * kMtN;  // the pad: a copy of A[0..15]
+constexpr int kMtWin = 16;              // most words a locking lane prefetches (WIN)
 __device__ __forceinline__ void mt_unpack(uint32_t r, int &idx, int &pg, int &cur) {
     idx = (int)(r & 0x3FFu);
     pg = (int)((r >> 10) & 0x3FFu);
@@ -283,34 +285,44 @@ __device__ __forceinline__ u32x4 mt_ld16(const MtRes &rs, bool on, uint32_t word
 // draw window cur[idx..idx+7] and the operands of the next block.  Reads past
 // an env's state land in the next env's state or the allocation's back pad.
 struct MtPre {
-    uint32_t w[8], a[5], x[4];
+    uint32_t w[kMtWin], a[5], x[4];
 };
+// WIN = 16 for st_step; 8 in rollouts, where the second half measured slower
+// (register pressure in the k-step loop).
+template <int WIN>
 __device__ __forceinline__ void mt_pre_load(const MtRes &rs, uint32_t mtst, bool want, MtPre &q) {
     int idx, pg, cur;
     mt_unpack(mtst, idx, pg, cur);
     const uint32_t cb = cur ? kMtB : 0u, nb = cur ? 0u : kMtB;
     const bool work = want && pg < kMtN;
-    const u32x4 w0 = mt_ld16(rs, want, cb + idx), w1 = mt_ld16(rs, want, cb + idx + 4);
+    u32x4 wv[WIN / 4];
+#pragma unroll
+    for (int i = 0; i < WIN / 4; ++i) wv[i] = mt_ld16(rs, want, cb + idx + 4 * i);
     const u32x4 a = mt_ld16(rs, work, cb + pg);
     const u32x4 x = mt_ld16(rs, work, pg <= 224 ? cb + pg + 397 : nb + pg - 227);
     q.a[4] = __builtin_amdgcn_raw_buffer_load_b32(rs.r, work ? rs.lane_off + 4u * (cb + pg + 4) : kOff, 0, 0);
-    q.w[0] = w0.x, q.w[1] = w0.y, q.w[2] = w0.z, q.w[3] = w0.w;
-    q.w[4] = w1.x, q.w[5] = w1.y, q.w[6] = w1.z, q.w[7] = w1.w;
+#pragma unroll
+    for (int i = 0; i < WIN / 4; ++i)
+        q.w[4 * i] = wv[i].x, q.w[4 * i + 1] = wv[i].y, q.w[4 * i + 2] = wv[i].z, q.w[4 * i + 3] = wv[i].w;
     q.a[0] = a.x, q.a[1] = a.y, q.a[2] = a.z, q.a[3] = a.w;
     q.x[0] = x.x, q.x[1] = x.y, q.x[2] = x.z, q.x[3] = x.w;
 }
 // Take all prefetched words at once (one vmcnt wait on a single path): words
 // never read would stay "pending" for the compiler, and every later reuse of
 // their registers would wait vmcnt(0), draining the step's early stores.
+template <int WIN>
 __device__ __forceinline__ void mt_pre_consume(const MtPre &q) {
     asm volatile("" ::"v"(q.w[0]), "v"(q.w[1]), "v"(q.w[2]), "v"(q.w[3]), "v"(q.w[4]), "v"(q.w[5]),
                  "v"(q.w[6]), "v"(q.w[7]));
+    if constexpr (WIN > 8)
+        asm volatile("" ::"v"(q.w[8]), "v"(q.w[9]), "v"(q.w[10]), "v"(q.w[11]), "v"(q.w[12]),
+                     "v"(q.w[13]), "v"(q.w[14]), "v"(q.w[15]));
     asm volatile("" ::"v"(q.a[0]), "v"(q.a[1]), "v"(q.a[2]), "v"(q.a[3]), "v"(q.a[4]), "v"(q.x[0]),
                  "v"(q.x[1]), "v"(q.x[2]), "v"(q.x[3]));
 }
 
 // One block of the next generation, next[p..p+3] (lanes with `want` and
-// p < 624), as one 16-B store (+ the pad copy for next = A, p = 0).
+// p < 624), as one 16-B store (+ the pad copy for next = A, p < 16).
 __device__ __forceinline__ void mt_work(const MtRes &rs, bool want, uint32_t &mtst, const MtPre &q) {
     int idx, pg, cur;
     mt_unpack(mtst, idx, pg, cur);
@@ -322,7 +334,7 @@ __device__ __forceinline__ void mt_work(const MtRes &rs, bool want, uint32_t &mt
     v.w = q.x[3] ^ mt_mix(q.a[3], q.a[4]);
     const uint32_t nb = cur ? 0u : kMtB;
     buf_store16(rs.r, work ? rs.lane_off + 4u * (nb + (uint32_t)pg) : kOff, v);
-    buf_store16(rs.r, work && cur && pg == 0 ? rs.lane_off + 4u * kMtPad : kOff, v);
+    buf_store16(rs.r, work && cur && pg < kMtWin ? rs.lane_off + 4u * (kMtPad + (uint32_t)pg) : kOff, v);
     if (work) mtst = mt_pack(idx, pg + 4, cur);
 }
 
@@ -369,7 +381,7 @@ __device__ void mt_finish(uint32_t *g, uint32_t *S, int lane, int pg, int cur) {
     wave_sync();
     for (int i = lane; i < kMtN; i += kWave)
         if (i >= pg) dst[i] = S[i];
-    if (cur && lane < 4) g[kMtPad + lane] = S[lane];
+    if (cur && lane < kMtWin) g[kMtPad + lane] = S[lane];
     __builtin_amdgcn_s_waitcnt(0);  // rare path: stores done before the wave reads them back
     wave_sync();
 }
@@ -383,6 +395,7 @@ __device__ void mt_finish(uint32_t *g, uint32_t *S, int lane, int pg, int cur) {
 // independent chains, each lane takes its first accepted one; lanes the
 // window does not settle (8 rejections, p <= 2^-8, or the generation's end)
 // continue in the loop, switching generations at index 624.
+template <int WIN>
 __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t &mtst,
                                           uint32_t *mt_wave, uint32_t *S, int lane,
                                           const MtPre &pre, bool have_pre) {
@@ -398,24 +411,45 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
     mt_unpack(mtst, idx, pg, cur);
     bool pending = need;
     uint32_t r = 0;
-    mt_pre_consume(pre);
+    mt_pre_consume<WIN>(pre);
     if (have_pre && pending) {
-        int first = 8;
-        uint32_t rr = 0;
+        // The prefetched words sit at positions idx.. of the current
+        // generation and, past 623, of the next one (cur[624..639] is
+        // next[0..15], see the layout) -- usable there once it is complete.
+        const int lim = pg == kMtN ? kMtN + WIN : kMtN;
+        int pos = idx;  // words consumed, counted from the current generation's start
+        auto pass = [&](int j0) {
+            int first = 8;
+            uint32_t rr = 0;
 #pragma unroll
-        for (int j = 7; j >= 0; --j) {
-            const uint32_t y = mt_temper(pre.w[j]) >> (32 - kb);
-            const bool acc = y < n && idx + j < kMtN;
-            first = acc ? j : first;
-            rr = acc ? y : rr;
+            for (int j = 7; j >= 0; --j) {
+                const uint32_t y = mt_temper(pre.w[j0 + j]) >> (32 - kb);
+                const bool acc = y < n && idx + j0 + j < lim;
+                first = acc ? j : first;
+                rr = acc ? y : rr;
+            }
+            if (first < 8) {
+                pending = false;
+                r = rr;
+                pos = idx + j0 + first + 1;
+            } else {
+                pos = idx + j0 + 8 < lim ? idx + j0 + 8 : lim;
+            }
+        };
+        pass(0);
+        // 8 rejections in a row (p <= 2^-8 per draw, a few lanes per step):
+        // the next 8 words are already here, no dependent load
+        if constexpr (WIN > 8) {
+            if (__ballot(pending && pos == idx + 8)) {
+                if (pending && pos == idx + 8) pass(8);
+            }
         }
-        if (first < 8) {
-            pending = false;
-            r = rr;
-            idx += first + 1;
-        } else {
-            idx = idx + 8 < kMtN ? idx + 8 : kMtN;
+        if (pos > kMtN) {  // the draw ran into the (complete) next generation
+            cur ^= 1;
+            pos -= kMtN;
+            pg = 0;
         }
+        idx = pos;
     }
     if (__ballot(pending)) {
         const MtRes rs = mt_res(mt_wave, lane);
@@ -660,7 +694,8 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     const bool want_pre = locknow && !(p.ablate & 2u);
     const MtRes mrs = mt_res(p.mt + e0 * kMtPitch, lane);
     MtPre pre;
-    mt_pre_load(mrs, mtst, want_pre, pre);
+    constexpr int kWin = KSTEPS == 1 ? 16 : 8;
+    mt_pre_load<kWin>(mrs, mtst, want_pre, pre);
 
     // ---- lock path (tetris_env.py:263-299) ----
     bool died = false, spawn = false;
@@ -810,9 +845,9 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         ST_STAMP(9);
     }
     if (!(p.ablate & 2u)) {
-        mt_pre_consume(pre);
+        mt_pre_consume<kWin>(pre);
         mt_work(mrs, want_pre, mtst, pre);  // before the draw: a switch it makes resets the progress
-        pick = draw_shape(draw, cnt, mtst, p.mt + e0 * kMtPitch, S, lane, pre, want_pre);
+        pick = draw_shape<kWin>(draw, cnt, mtst, p.mt + e0 * kMtPitch, S, lane, pre, want_pre);
     }
     ST_STAMP(4);
     if constexpr (STAMP) {  // 1: a draw started a generation, 2: a draw ran past its 8 words
@@ -1017,7 +1052,7 @@ __global__ __launch_bounds__(kWave) void k_reset(KParams p) {
     uint32_t mtst = (uint32_t)st[ST_STAT_MT_INDEX * sd];
     const uint32_t pw = p.piece[e];
     const MtPre nopre{};
-    const int pick = draw_shape(m, cnt, mtst, p.mt + e0 * kMtPitch, S, lane, nopre, false);
+    const int pick = draw_shape<8>(m, cnt, mtst, p.mt + e0 * kMtPitch, S, lane, nopre, false);
     if (m) {
         st[ST_STAT_TIME * sd] = 0;
         st[ST_STAT_SCORE * sd] = 0;

@@ -361,9 +361,10 @@ def _untemper(y):
 
 @pytest.mark.parametrize("mode", ["step", "rollout"])
 def test_long_rejection_runs_and_twists(mode):
-    """Crafted MT states: draws that reject 20 words in a row (past the
-    8-word prefetch and the 16-word ring), and states 1-3 words from a twist,
-    against the oracle with the same states."""
+    """Crafted MT states: draws that reject 10 words in a row (the second
+    half of the 16-word prefetch), 20 (past it: the dependent-load loop), and
+    states 1-3 words from a generation's end whose successor is not built
+    (host-written state: finished cooperatively), against the oracle."""
     G = _engine()
     n, T = 64, 40
     b = G.TetrisBatch(n, autoreset="same_step", seeds=range(n))
@@ -386,6 +387,9 @@ def test_long_rejection_runs_and_twists(mode):
             mt[i, idx + 18] = acc
             mt[i, idx + 19:idx + 40] = rej
             mt[i, idx + 40] = acc
+        elif i % 4 == 3 and idx + 11 <= 624:         # 10 rejections: the second prefetched half
+            mt[i, idx:idx + 10] = rej
+            mt[i, idx + 10] = acc
         e = ob.envs[i]
         for k in range(624):
             e.rng.mt[k] = int(mt[i, k])
