@@ -121,9 +121,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uin
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, base ? (int)bytes : 0,
                                              0x00020000);
 }
+// Cache policy of the step's stores: non-temporal (gfx950 `nt`).  Lines a
+// store leaves dirty in L2 are written back at the kernel's end, on the
+// dependent launch's critical path (the guide's boundary cost + B / 6 TB/s);
+// `nt` stores stream out during the kernel instead (A/B, st_step packed:
+// 6.31 -> 5.89 us with obs, board, counter and MT stores all `nt`).
+constexpr int kNT = 2;
+template <int AUX = 0>
 __device__ __forceinline__ void buf_store16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
     const i32x4 d = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
-    __builtin_amdgcn_raw_buffer_store_b128(d, r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(d, r, off, 0, AUX);
 }
 
 __device__ __forceinline__ uint32_t &lcol(uint32_t *L, int x, int lane) {
@@ -323,6 +330,9 @@ __device__ __forceinline__ void mt_pre_consume(const MtPre &q) {
 
 // One block of the next generation, next[p..p+3] (lanes with `want` and
 // p < 624), as one 16-B store (+ the pad copy for next = A, p < 16).
+// AUX: kNT in st_step; plain in rollouts, whose later steps re-read the
+// blocks (X operands, the switch) from L2.
+template <int AUX>
 __device__ __forceinline__ void mt_work(const MtRes &rs, bool want, uint32_t &mtst, const MtPre &q) {
     int idx, pg, cur;
     mt_unpack(mtst, idx, pg, cur);
@@ -333,8 +343,8 @@ __device__ __forceinline__ void mt_work(const MtRes &rs, bool want, uint32_t &mt
     v.z = q.x[2] ^ mt_mix(q.a[2], q.a[3]);
     v.w = q.x[3] ^ mt_mix(q.a[3], q.a[4]);
     const uint32_t nb = cur ? 0u : kMtB;
-    buf_store16(rs.r, work ? rs.lane_off + 4u * (nb + (uint32_t)pg) : kOff, v);
-    buf_store16(rs.r, work && cur && pg < kMtWin ? rs.lane_off + 4u * (kMtPad + (uint32_t)pg) : kOff, v);
+    buf_store16<AUX>(rs.r, work ? rs.lane_off + 4u * (nb + (uint32_t)pg) : kOff, v);
+    buf_store16<AUX>(rs.r, work && cur && pg < kMtWin ? rs.lane_off + 4u * (kMtPad + (uint32_t)pg) : kOff, v);
     if (work) mtst = mt_pack(idx, pg + 4, cur);
 }
 
@@ -826,7 +836,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
                 v.w &= km.w;
                 // row 4q + lrow; padding rows (>= W) are never dirty
                 const bool dirty = (bdl >> (4 * q)) & 1u && 4 * q + lrow < W;
-                buf_store16(rb, dirty ? boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff, v);
+                buf_store16<kNT>(rb, dirty ? boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff, v);
             }
         }
         wave_sync();  // the board reads above precede the overlay paint
@@ -846,7 +856,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     }
     if (!(p.ablate & 2u)) {
         mt_pre_consume<kWin>(pre);
-        mt_work(mrs, want_pre, mtst, pre);  // before the draw: a switch it makes resets the progress
+        mt_work<KSTEPS == 1 ? kNT : 0>(mrs, want_pre, mtst, pre);  // before the draw: a switch it makes resets the progress
         pick = draw_shape<kWin>(draw, cnt, mtst, p.mt + e0 * kMtPitch, S, lane, pre, want_pre);
     }
     ST_STAMP(4);
@@ -903,7 +913,6 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     if (obs_t && !(p.ablate & 8u)) {
         if (wide_obs) {
             const uint32_t noff = (uint32_t)lrow * (uint32_t)p.n + (uint32_t)lcc;
-            uint32_t *odst = obs_t + e0;
 #pragma unroll
             for (int q = 0; q < NBQ; ++q) {  // interleaved read/store (measured: reads-first
                                              // costs the packed rollout ~7%)
@@ -913,7 +922,8 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
                     v.y &= hmask;
                     v.z &= hmask;
                     v.w &= hmask;
-                    *reinterpret_cast<uint4 *>(odst + (size_t)(4 * q) * p.n + noff) = v;
+buf_store16<kNT>(buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u),
+                                     ((uint32_t)e0 + (uint32_t)(4 * q) * (uint32_t)p.n + noff) * 4u, v);
                 }
             }
         } else if (real) {
@@ -944,7 +954,8 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
                 if constexpr (KSTEPS != 1) {
                     // rollouts: non-temporal (A/B: -13% f32 rollout; the MT and
                     // state lines stay in L2 instead of the streamed obs; +7% on
-                    // the single-step launch, so not there)
+                    // the single-step launch before its other stores were
+                    // made nt, +-0 after, so it keeps plain stores)
                     typedef float f32x4 __attribute__((ext_vector_type(4)));
                     const f32x4 fv = {f.x, f.y, f.z, f.w};
                     __builtin_nontemporal_store(fv, reinterpret_cast<f32x4 *>(&out4[c]));
@@ -1006,7 +1017,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     for (int q = 0; q < kHotQ; ++q) {
         // row 15 (ep_time) is never staged: it is stored per lane on a reset
         const bool st = 4 * q + lrow < kHotRows && ((sdl >> (4 * q)) & 1u);
-        buf_store16(rs, st ? soff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff,
+        buf_store16<kNT>(rs, st ? soff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff,
                     *reinterpret_cast<const uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]));
     }
     if constexpr (STAMP && KSTEPS == 1) {
