@@ -325,6 +325,44 @@ def main():
                 "roofline": roofline(ev / nch, rollout_bytes(W, H, pl, use_f32, CH), CH,
                                      f"k_rollout<10, 20, {'true' if use_f32 else 'false'}>")}
             del rf
+        # Clear-heavy regime: uniform actions almost never clear
+        # a line, so the same st_step is also timed on an action stream that
+        # a greedy placement player (st_policy_greedy, 3% random) produced from
+        # the same start state: recorded untimed, then replayed from a
+        # snapshot of that start state through the same hipGraph path.
+        ce = ShardedTetris(n_global, seed=1000, rank=rank, world=world, device=dev,
+                           autoreset="same_step", width=W, height=H, **cfg_kw).engine
+        ce.reset()
+        snap = ce.save()
+        gact = torch.empty((WU + K, n_local), dtype=torch.uint8, device=dev)
+        cleared = torch.zeros((), dtype=torch.int64, device=dev)
+        with torch.cuda.stream(s):
+            for t in range(WU + K):
+                ce.policy_greedy(t, seed=aseed, explore=30, out=gact[t])
+                C.check(L.st_step(ce._ctx, ctypes.c_void_p(gact[t].data_ptr()), p_obs, p_rew, p_done, sp))
+                if t >= WU:  # default rewards: +100 per cleared line
+                    cleared += rew_v.clamp(min=0).sum()
+        torch.cuda.synchronize(dev)
+        n_cleared = int(cleared.item())
+        ce.load(snap)
+        del snap
+        gptr = [ctypes.c_void_p(gact[t].data_ptr()) for t in range(WU + K)]
+        with torch.cuda.stream(s):
+            for t in range(WU):
+                C.check(L.st_step(ce._ctx, gptr[t], p_obs, p_rew, p_done, sp))
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for t in range(WU, WU + K):
+                C.check(L.st_step(ce._ctx, gptr[t], p_obs, p_rew, p_done, sp))
+        torch.cuda.synchronize(dev)
+        el, ev, _ = timed(g.replay, K)
+        variants["step_clear_heavy"] = {
+            "value": n_global * K / el, "ms_per_step": el / K * 1e3,
+            "lines_per_env_step": (n_cleared / 100.0 / (n_local * K)) if args.config == "c3" else None,
+            "actions": "st_policy_greedy (greedy placement, 3% uniform), recorded then replayed",
+            "kernel_us": ev / K * 1e3}
+        del g, ce
         out["variants"] = variants
         if args.gather and world > 1:
             torch.cuda.synchronize(dev)

@@ -380,6 +380,16 @@ int st_debug_stamps(st_ctx *c, uint64_t *host_out, int64_t max_words) {
     return ST_OK;
 }
 
+int st_policy_greedy(st_ctx *c, uint64_t seed, int64_t t, uint32_t explore_permille, uint8_t *d_actions,
+                     st_stream stream) {
+    if (!c || !d_actions) return fail(ST_EINVAL, "st_policy_greedy: null argument");
+    if (t < 0 || explore_permille > 1000) return fail(ST_EINVAL, "st_policy_greedy: t < 0 or explore > 1000");
+    if (!c->seeded || !c->reset_once) return fail(ST_ESTATE, "st_policy_greedy before st_seed + st_reset");
+    DeviceGuard g(c->device);
+    ST_HIP(st::launch_policy_greedy(params(c), seed, t, explore_permille, d_actions, (hipStream_t)stream));
+    return ST_OK;
+}
+
 int st_gen_actions(uint8_t *d_out, int64_t n, int64_t t, uint64_t seed, int64_t global_offset,
                    st_stream stream) {
     if (!d_out && n > 0) return fail(ST_EINVAL, "st_gen_actions: null output");

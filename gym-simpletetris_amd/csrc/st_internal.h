@@ -59,6 +59,8 @@ hipError_t launch_rollout(const KParams &p, hipStream_t s);
 hipError_t launch_obs_f32(const KParams &p, const uint32_t *obs, float *out, hipStream_t s);
 hipError_t launch_render(const KParams &p, hipStream_t s);
 hipError_t launch_mt_sync(const KParams &p, hipStream_t s);
+hipError_t launch_policy_greedy(const KParams &p, uint64_t seed, int64_t t, uint32_t explore,
+                                uint8_t *out, hipStream_t s);
 hipError_t launch_grayscale(const KParams &p, const uint32_t *obs, int size, int channels,
                             int as_u8, void *out, hipStream_t s);
 hipError_t launch_gen_actions(uint8_t *out, int64_t n, int64_t t, uint64_t seed, int64_t off,

@@ -1253,6 +1253,89 @@ __global__ void k_gen_actions(uint8_t *out, int64_t n, int64_t t, uint64_t seed,
     out[e] = (uint8_t)(splitmix64(x) % 7ull);
 }
 
+// ---------------------------------------------------------------- greedy policy
+// Benchmark / test workload generator (not part of the reference env): the
+// action a greedy placement player takes in every env's current state, so
+// that rollouts clear lines (uniform random actions almost never do; SURVEY
+// §8(d) asks for a clear-heavy variant).  For the current piece, every
+// (rot 0..3, anchor x in [-3, W+3)) is hard-dropped from row 0 onto the
+// board; score = 80*lines - 12*holes - 3*height - 2000*(piece above the top)
+// (2 x the fixture generator's 40 / 6 / 1.5 / 1000, tests/golden/gen_golden.py
+// greedy_target), first maximum in (rot, x) order.  The action turns the
+// piece toward the target rotation (rotate_left), then moves it toward x,
+// then hard-drops; with probability explore/1000 it is a uniform random
+// action instead: splitmix64(seed ^ (t << 32 ^ e)).  Stateless: the target
+// depends only on the board and the piece id.
+__global__ __launch_bounds__(kWave) void k_policy_greedy(KParams p, uint64_t seed, int64_t t,
+                                                         uint32_t explore, uint8_t *out) {
+    constexpr int P = 8;  // wall columns each side: x + dx spans [-6, W + 5]
+    __shared__ uint32_t L[(kMaxW + 2 * P) * kWave];
+    const int lane = threadIdx.x;
+    const int64_t e = (int64_t)blockIdx.x * kWave + lane;
+    const int64_t sd = p.stride;
+    const int W = p.W, H = p.H;
+    const uint32_t hmask = (1u << H) - 1u, floorb = ~hmask;
+    auto col = [&](int c) -> uint32_t & { return L[(c + P) * kWave + lane]; };
+    for (int c = 0; c < W; ++c) col(c) = p.board[c * sd + e] | floorb;
+    for (int c = 0; c < P; ++c) {
+        col(c - P) = ~0u;
+        col(W + c) = ~0u;
+    }
+    const uint32_t pw = p.piece[e];
+    const int id = (int)(pw & 7u), rot = (int)((pw >> 3) & 3u), ax = (int)((pw >> 5) & 63u);
+    int best_score = INT32_MIN, trot = -1, tx = 0;
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t m = c_tab_m[id * 4 + r], g = c_tab_g[id * 4 + r];
+        for (int x = -3; x < W + 3; ++x) {
+            uint32_t v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = col(x + pc_dx(g, j));
+            if (collides_v(m, 0, v)) continue;
+            const int y = drop_v(g, 0, v);
+            bool ok = true;
+            uint32_t pb[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t byte = (m >> (8 * j)) & 0xFFu;
+                ok = ok && y + __builtin_ctz(byte) - 3 >= 0;
+                pb[j] = pc_bits(m, j, y) & hmask;
+            }
+            // the board with the piece: column c gets the bits of every
+            // descriptor column at c (repeated last columns are idempotent)
+            uint32_t andv = hmask;
+            for (int c = 0; c < W; ++c) {
+                uint32_t w = col(c);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) w |= x + pc_dx(g, j) == c ? pb[j] : 0u;
+                andv &= w;
+            }
+            const int lines = __builtin_popcount(andv);
+            int holes = 0;
+            uint32_t orv = 0;
+            for (int c = 0; c < W; ++c) {
+                uint32_t w = col(c);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) w |= x + pc_dx(g, j) == c ? pb[j] : 0u;
+                w = (andv ? compact(w & hmask, andv) : (w & hmask)) | floorb;
+                holes += H - (int)__builtin_ctz(w) - __builtin_popcount(w & hmask);
+                orv |= w & hmask;
+            }
+            const int height = orv ? H - (int)__builtin_ctz(orv) : 0;
+            const int sc = 80 * lines - 12 * holes - 3 * height - (ok ? 0 : 2000);
+            if (sc > best_score) {
+                best_score = sc;
+                trot = r;
+                tx = x;
+            }
+        }
+    }
+    uint32_t a = 2u;  // no legal placement: hard drop
+    if (trot >= 0) a = rot != trot ? 4u : (ax < tx ? 1u : (ax > tx ? 0u : 2u));
+    const uint64_t h = splitmix64(seed ^ (((uint64_t)t << 32) ^ (uint64_t)e));
+    if ((uint32_t)(h % 1000ull) < explore) a = (uint32_t)((h >> 32) % 7ull);
+    if (e < p.n) out[e] = (uint8_t)a;
+}
+
 }  // namespace
 
 hipError_t launch_seed(const KParams &p, hipStream_t s) {
@@ -1325,6 +1408,13 @@ hipError_t launch_grayscale(const KParams &p, const uint32_t *obs, int size, int
     else
         hipLaunchKernelGGL(k_grayscale<float>, dim3((unsigned)blocks), dim3(256), 0, s, obs,
                            (float *)out, p.n, p.W, p.H, size, channels);
+    return hipGetLastError();
+}
+
+hipError_t launch_policy_greedy(const KParams &p, uint64_t seed, int64_t t, uint32_t explore,
+                                uint8_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_policy_greedy, dim3((unsigned)(p.stride / kWave)), dim3(kWave), 0, s, p, seed, t,
+                       explore, out);
     return hipGetLastError();
 }
 

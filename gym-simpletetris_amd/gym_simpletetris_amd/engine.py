@@ -314,6 +314,18 @@ class TetrisBatch:
                     ep_time=st[C.STAT["ep_time"]], ep_score=st[C.STAT["ep_score"]],
                     ep_lines=st[C.STAT["ep_lines"]], ep_holes=st[C.STAT["ep_holes"]])
 
+    def policy_greedy(self, t: int, seed: int = 0, explore: int = 30,
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Greedy placement actions for the current states (st_policy_greedy):
+        a clear-heavy workload generator for benchmarks and tests; `explore`
+        per mille of the actions are uniform random (splitmix64 keyed by
+        seed, t and the env index)."""
+        out = self._act if out is None else out
+        with torch.cuda.device(self.device):
+            C.check(self._L.st_policy_greedy(self._ctx, ctypes.c_uint64(seed), int(t), int(explore),
+                                             _ptr(out), self._stream()))
+        return out
+
     def gen_actions(self, t: int, seed: int, global_offset: int = 0,
                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Synthetic uniform actions splitmix64(seed ^ ((t<<32) ^ e)) % 7 on device."""

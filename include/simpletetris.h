@@ -210,6 +210,18 @@ int64_t st_state_bytes(const st_ctx *ctx);
 int st_save(st_ctx *ctx, void *host_out, int64_t bytes);
 int st_load(st_ctx *ctx, const void *host_in, int64_t bytes);
 
+/* Greedy placement policy (a benchmark / test workload generator, not part
+ * of the reference env; SURVEY 8(d) "clear-heavy variant"): d_actions[e] =
+ * the action a greedy player takes in env e's current state -- rotate_left
+ * toward, then move toward, then hard-drop onto the placement maximizing
+ * 80*lines - 12*holes - 3*height - 2000*(piece above the top) over all
+ * (rotation, anchor x) hard-dropped from row 0 (first maximum in rotation,
+ * then x order) -- or, with probability explore_permille/1000, the uniform
+ * action splitmix64(seed ^ ((t << 32) ^ e)) >> 32 mod 7.  Reads the state
+ * enqueued before it on `stream`. */
+int st_policy_greedy(st_ctx *ctx, uint64_t seed, int64_t t, uint32_t explore_permille,
+                     uint8_t *d_actions, st_stream stream);
+
 /* Synthetic action source used by the benchmark and the parity tests:
  * d_out[e] = splitmix64(seed ^ ((t << 32) ^ (global_offset + e))) % 7. */
 int st_gen_actions(uint8_t *d_out, int64_t n, int64_t t, uint64_t seed,

@@ -462,6 +462,87 @@ def test_mt_generations_across_steps():
         assert np.array_equal(fa["mt"][i], np.ctypeslib.as_array(ob.envs[i].rng.mt)), i
 
 
+def _greedy_ref(col_words, W, H, pw):
+    """numpy restatement of st_policy_greedy with explore = 0 (the fixture
+    generator's greedy_target / greedy_action, tests/golden/gen_golden.py,
+    scores doubled to integers)."""
+    board = ((np.asarray(col_words, np.uint64)[:, None] >> np.arange(H, dtype=np.uint64)) & 1).astype(bool)
+    sid, rot, ax = pw & 7, (pw >> 3) & 3, (pw >> 5) & 63
+    best, best_s = None, None
+    for r in range(4):
+        cells = O.rotate_cells(O.BASE_SHAPES[sid], r)
+
+        def occ(x0, y0):
+            for i, j in cells:
+                x, y = x0 + i, y0 + j
+                if y < 0:
+                    continue
+                if x < 0 or x >= W or y >= H or board[x, y]:
+                    return True
+            return False
+        for x in range(-3, W + 3):
+            if occ(x, 0):
+                continue
+            y = 0
+            while not occ(x, y + 1):
+                y += 1
+            b, ok = board.copy(), True
+            for i, j in cells:
+                if 0 <= x + i < W and 0 <= y + j < H:
+                    b[x + i, y + j] = True
+                elif y + j < 0:
+                    ok = False
+            full = np.all(b, axis=0)
+            keep = b[:, ~full]
+            nb = np.zeros_like(b)
+            nb[:, H - keep.shape[1]:] = keep
+            holes = int(np.count_nonzero(nb.cumsum(axis=1) * ~nb))
+            fr = np.any(nb, axis=0)
+            height = H - int(np.argmax(fr)) if fr.any() else 0
+            sc = 80 * int(full.sum()) - 12 * holes - 3 * height - (0 if ok else 2000)
+            if best_s is None or sc > best_s:
+                best_s, best = sc, (r, x)
+    if best is None:
+        return 2
+    if rot != best[0]:
+        return 4
+    return 1 if ax < best[1] else (0 if ax > best[1] else 2)
+
+
+def test_greedy_policy_and_clear_heavy_parity():
+    """st_policy_greedy against its numpy restatement on evolving states, and
+    the clear-heavy trajectory it drives against the oracle (bit-exact, with
+    line clears at every count the boards produce)."""
+    G = _engine()
+    n, T, W, H = 128, 240, 10, 20
+    seeds = [21 + e for e in range(n)]
+    kw = dict(width=W, height=H, advanced_clears=True, penalise_holes_increase=True,
+              penalise_height_increase=True)
+    b = G.TetrisBatch(n, autoreset="same_step", seeds=seeds, **kw)
+    b.reset()
+    acts = np.zeros((T, n), np.uint8)
+    for t in range(T):
+        if t % 40 == 7:  # the policy itself, explore off, vs numpy
+            a0 = b.policy_greedy(t, seed=3, explore=0).cpu().numpy().copy()
+            st = b.get_state(("board", "piece"))
+            for e in range(0, n, 5):
+                assert int(a0[e]) == _greedy_ref(st["board"][:, e], W, H, int(st["piece"][e])), (t, e)
+        a = b.policy_greedy(t, seed=3, explore=30)
+        acts[t] = a.cpu().numpy()
+        b.step(a)
+    ob = O.OracleBatch(n, seeds, **kw)
+    ob.reset()
+    ref = ob.rollout(acts)
+    c = G.TetrisBatch(n, autoreset="same_step", seeds=seeds, **kw)
+    c.reset()
+    obs, rew, done = c.rollout(torch.as_tensor(acts, device=c.device))
+    assert np.array_equal(rew.cpu().numpy(), ref["reward"])
+    assert np.array_equal(done.cpu().numpy().astype(np.uint8), ref["done"])
+    assert np.array_equal(obs.cpu().numpy().view(np.uint32).transpose(0, 2, 1), ref["obs"])
+    lines = c.info_tensors()["lines_cleared"].cpu().numpy()
+    assert lines.sum() > n  # the point of the policy: many clears
+
+
 def test_abi_error_paths():
     """The C ABI rejects bad arguments and call-order violations with codes
     and a message instead of faulting (reference: exceptions)."""
