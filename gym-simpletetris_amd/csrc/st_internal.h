@@ -29,7 +29,8 @@ struct KParams {
     int32_t lock_mod;   // max(lock_delay, 0) + 1   (tetris_env.py:175)
     uint32_t flags;
     int32_t autoreset;
-    uint32_t ablate;    // TIMING DIAGNOSTICS ONLY (env ST_ABLATE at st_create); 0 in
+    uint32_t ablate;    // TIMING DIAGNOSTICS ONLY (env ST_ABLATE at st_create, read only by
+                        // -DST_ABLATION=1 builds, tools/ablate.sh); 0 in
                         // every correct run: 1 = no lock path, 2 = no MT draw,
                         // 4 = no twist, 8 = no obs output
     uint64_t *stamps;   // DIAGNOSTIC build only (env ST_STAMPS at st_create): per-wave

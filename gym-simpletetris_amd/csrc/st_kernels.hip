@@ -533,11 +533,25 @@ __device__ __forceinline__ uint32_t pack_piece(int id, int rot, int ax, int ay, 
 // KSTEPS == 0: p.k consecutive steps (st_rollout) with the board and counters
 // kept in LDS between steps, actions read one step ahead, and per-step
 // outputs at [t].  State is loaded once at the start and stored once at the end.
-template <int WT, int HT, bool F32, bool STAMP, int KSTEPS>
+// SC0: the context has no scoring flags (the reference's defaults,
+// tetris_env.py:126-137): those tests fold away at compile time (measured:
+// the rollout loop otherwise holds each flag as a 64-bit lane mask at the
+// SGPR limit, -5% packed rollout; st_step -1%).
+template <int WT, int HT, bool F32, bool STAMP, int KSTEPS, bool SC0 = false>
 __device__ __forceinline__ void run_steps(const KParams &p) {
     [[maybe_unused]] uint64_t tstamp[10] = {};
     [[maybe_unused]] uint64_t draw_kind = 0;  // stamp build: 1 = a lane twisted, 2 = a draw ran past 8 words
     constexpr bool S32 = HT != 0 && HT <= 25;  // see pc_bits
+    const uint32_t kFlags = SC0 ? (p.flags & (ST_REWARD_STEP | ST_STEP_RESET)) : p.flags;
+
+    // timing ablations (tools/ablate.sh) exist only in -DST_ABLATION=1 builds:
+    // as runtime flags each costs two SGPRs of lane masks, and the rollout
+    // loop is at the SGPR limit
+#if defined(ST_ABLATION) && ST_ABLATION
+    const uint32_t kAblate = p.ablate;
+#else
+    constexpr uint32_t kAblate = 0u;
+#endif
     [[maybe_unused]] uint64_t rt0 = 0;
     if constexpr (STAMP) rt0 = __builtin_amdgcn_s_memrealtime();
     ST_STAMP(0);
@@ -686,22 +700,22 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     if (d > 0) {
         ay += 1;
         d -= 1;
-        if (p.flags & ST_STEP_RESET) lock = 0;
+        if (kFlags & ST_STEP_RESET) lock = 0;
     }
     time += 1;
-    int32_t rew = (p.flags & ST_REWARD_STEP) ? 1 : 0;
+    int32_t rew = (kFlags & ST_REWARD_STEP) ? 1 : 0;
     bool locknow = false;
     if (d == 0) {
         const int l1 = lock + 1;  // (x + 1) % lock_mod; x < lock_mod unless set_state said otherwise
         lock = l1 < p.lock_mod ? l1 : (l1 == p.lock_mod ? 0 : l1 % p.lock_mod);
-        locknow = lock == 0 && !(p.ablate & 1u);
+        locknow = lock == 0 && !(kAblate & 1u);
     }
     ST_STAMP(2);
     // MT window for the piece this lock will draw: issued now, consumed after
     // the lock path (every locking lane draws: a spawn, or the same-step
     // reset's), and the operands of its next-generation block (mt_work).
     uint32_t mtst = ss(ST_STAT_MT_INDEX);  // packed (mt_pack)
-    const bool want_pre = locknow && !(p.ablate & 2u);
+    const bool want_pre = locknow && !(kAblate & 2u);
     const MtRes mrs = mt_res(p.mt + e0 * kMtPitch, lane);
     MtPre pre;
     constexpr int kWin = KSTEPS == 1 ? 16 : 8;
@@ -753,14 +767,14 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         }
         orv &= hmask;
         const int32_t nh = W * H - (int32_t)sctz - ((int32_t)spop - W * (32 - H));
-        if (p.flags & ST_ADVANCED_CLEARS) {  // :266-269, 2.5 * [0,40,100,300,1200]
+        if (kFlags & ST_ADVANCED_CLEARS) {  // :266-269, 2.5 * [0,40,100,300,1200]
             // [0, 40, 100, 300, 1200][ncl] as 12-bit fields of one constant
             // (ncl > 4 only from a crafted set_state board: 0, as before)
             constexpr uint64_t kClr = (40ull << 12) | (100ull << 24) | (300ull << 36) | (1200ull << 48);
             const int32_t sc = ncl <= 4 ? (int32_t)((kClr >> (12 * ncl)) & 0xFFFu) : 0;
             rew += (sc * 5) / 2;
             score += sc;
-        } else if (p.flags & ST_HIGH_SCORING) {  // :270-272
+        } else if (kFlags & ST_HIGH_SCORING) {  // :270-272
             rew += 1000 * ncl;
             score += ncl;
         } else {  // :273-275
@@ -776,14 +790,14 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
             const int32_t old_holes = holes;
             holes = nh;
             const int32_t hgt = __builtin_popcount(orv);  // sum(np.any(board, axis=0))
-            if (p.flags & ST_PENALISE_HEIGHT) {
+            if (kFlags & ST_PENALISE_HEIGHT) {
                 rew -= hgt;
-            } else if (p.flags & ST_PENALISE_HEIGHT_INCREASE) {
+            } else if (kFlags & ST_PENALISE_HEIGHT_INCREASE) {
                 if (hgt > height) rew -= 10 * (hgt - height);
                 height = hgt;
             }
-            if (p.flags & ST_PENALISE_HOLES) rew -= 5 * holes;
-            else if (p.flags & ST_PENALISE_HOLES_INCREASE) rew -= 5 * (holes - old_holes);
+            if (kFlags & ST_PENALISE_HOLES) rew -= 5 * holes;
+            else if (kFlags & ST_PENALISE_HOLES_INCREASE) rew -= 5 * (holes - old_holes);
             spawn = true;
         }
     }
@@ -854,7 +868,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         ST_STAMP(9);
     }
-    if (!(p.ablate & 2u)) {
+    if (!(kAblate & 2u)) {
         mt_pre_consume<kWin>(pre);
         mt_work<KSTEPS == 1 ? kNT : 0>(mrs, want_pre, mtst, pre);  // before the draw: a switch it makes resets the progress
         pick = draw_shape<kWin>(draw, cnt, mtst, p.mt + e0 * kMtPitch, S, lane, pre, want_pre);
@@ -910,7 +924,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     wave_sync();
     const bool wide_obs = (p.n & 3) == 0 && e0 + kWave <= p.n &&
                           (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0;
-    if (obs_t && !(p.ablate & 8u)) {
+    if (obs_t && !(kAblate & 8u)) {
         if (wide_obs) {
             const uint32_t noff = (uint32_t)lrow * (uint32_t)p.n + (uint32_t)lcc;
 #pragma unroll
@@ -922,7 +936,7 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
                     v.y &= hmask;
                     v.z &= hmask;
                     v.w &= hmask;
-buf_store16<kNT>(buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u),
+                    buf_store16<kNT>(buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u),
                                      ((uint32_t)e0 + (uint32_t)(4 * q) * (uint32_t)p.n + noff) * 4u, v);
                 }
             }
@@ -991,7 +1005,10 @@ buf_store16<kNT>(buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u),
     }  // for t
     wave_sync();
     if constexpr (KSTEPS != 1) {
-        uint32_t *bdst = p.board + e0;
+        // 32-bit buffer offsets: 64-bit row offsets shared with the prologue
+        // would stay live (in SGPRs) across the step loop
+        const auto rb = buf_rsrc(p.board, (uint32_t)((W + 3) & ~3) * (uint32_t)sd * 4u);
+        const uint32_t boff = (uint32_t)e0 * 4u + loff * 4u;
 #pragma unroll
         for (int q = 0; q < NBQ; ++q) {
             if (WT || 4 * q < W) {  // rows >= W: padding rows of the allocation
@@ -1000,11 +1017,10 @@ buf_store16<kNT>(buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u),
                 v.y &= hmask;
                 v.z &= hmask;
                 v.w &= hmask;
-                *reinterpret_cast<uint4 *>(bdst + (size_t)(4 * q) * sd + loff) = v;
+                buf_store16<kNT>(rb, boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u, v);
             }
         }
     }
-    uint32_t *sdst = reinterpret_cast<uint32_t *>(p.stats) + e0;
     uint32_t sdl = ~0u;  // rows to store: all (rollout) or those one of the lane's 4 envs changed
     if constexpr (KSTEPS == 1) {
         const uint4 sd4 = *reinterpret_cast<const uint4 *>(&SD[lcc]);
@@ -1012,7 +1028,6 @@ buf_store16<kNT>(buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u),
     }
     const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
     const uint32_t soff = (uint32_t)e0 * 4u + loff * 4u;
-    (void)sdst;
 #pragma unroll
     for (int q = 0; q < kHotQ; ++q) {
         // row 15 (ep_time) is never staged: it is stored per lane on a reset
@@ -1036,15 +1051,20 @@ buf_store16<kNT>(buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u),
     }
 }
 
-template <int WT, int HT, bool F32, bool STAMP = false>
+template <int WT, int HT, bool F32, bool STAMP = false, bool SC0 = false>
 __global__ __launch_bounds__(kWave) void k_step(KParams p) {
-    run_steps<WT, HT, F32, STAMP, 1>(p);
+    run_steps<WT, HT, F32, STAMP, 1, SC0>(p);
 }
 
-template <int WT, int HT, bool F32>
+template <int WT, int HT, bool F32, bool SC0 = false>
 __global__ __launch_bounds__(kWave) void k_rollout(KParams p) {
-    run_steps<WT, HT, F32, false, 0>(p);
+    run_steps<WT, HT, F32, false, 0, SC0>(p);
 }
+
+// no scoring flags (SC0 specializations of the 10x20 kernels)
+constexpr uint32_t kScoringFlags =
+    ST_PENALISE_HEIGHT | ST_PENALISE_HEIGHT_INCREASE | ST_ADVANCED_CLEARS | ST_HIGH_SCORING |
+    ST_PENALISE_HOLES | ST_PENALISE_HOLES_INCREASE;
 
 // ---------------------------------------------------------------- reset
 // TetrisEngine.clear (tetris_env.py:306-315) on masked envs.  n_deaths,
@@ -1352,11 +1372,15 @@ hipError_t launch_reset(const KParams &p, hipStream_t s) {
 hipError_t launch_step(const KParams &p, hipStream_t s) {
     const dim3 grid((unsigned)(p.stride / kWave)), block(kWave);
     const bool f32 = p.obs_f32 != nullptr;
+    const bool sc0 = !(p.flags & kScoringFlags);
     if (p.stamps && p.W == 10 && p.H == 20) {
         if (f32) hipLaunchKernelGGL((k_step<10, 20, true, true>), grid, block, 0, s, p);
+        else if (sc0) hipLaunchKernelGGL((k_step<10, 20, false, true, true>), grid, block, 0, s, p);
         else hipLaunchKernelGGL((k_step<10, 20, false, true>), grid, block, 0, s, p);
     } else if (p.W == 10 && p.H == 20) {
-        if (f32) hipLaunchKernelGGL((k_step<10, 20, true>), grid, block, 0, s, p);
+        if (f32 && sc0) hipLaunchKernelGGL((k_step<10, 20, true, false, true>), grid, block, 0, s, p);
+        else if (f32) hipLaunchKernelGGL((k_step<10, 20, true>), grid, block, 0, s, p);
+        else if (sc0) hipLaunchKernelGGL((k_step<10, 20, false, false, true>), grid, block, 0, s, p);
         else hipLaunchKernelGGL((k_step<10, 20, false>), grid, block, 0, s, p);
     } else {
         if (f32) hipLaunchKernelGGL((k_step<0, 0, true>), grid, block, 0, s, p);
@@ -1378,8 +1402,11 @@ hipError_t launch_render(const KParams &p, hipStream_t s) {
 hipError_t launch_rollout(const KParams &p, hipStream_t s) {
     const dim3 grid((unsigned)(p.stride / kWave)), block(kWave);
     const bool f32 = p.obs_f32 != nullptr;
+    const bool sc0 = !(p.flags & kScoringFlags);
     if (p.W == 10 && p.H == 20) {
-        if (f32) hipLaunchKernelGGL((k_rollout<10, 20, true>), grid, block, 0, s, p);
+        if (f32 && sc0) hipLaunchKernelGGL((k_rollout<10, 20, true, true>), grid, block, 0, s, p);
+        else if (f32) hipLaunchKernelGGL((k_rollout<10, 20, true>), grid, block, 0, s, p);
+        else if (sc0) hipLaunchKernelGGL((k_rollout<10, 20, false, true>), grid, block, 0, s, p);
         else hipLaunchKernelGGL((k_rollout<10, 20, false>), grid, block, 0, s, p);
     } else {
         if (f32) hipLaunchKernelGGL((k_rollout<0, 0, true>), grid, block, 0, s, p);

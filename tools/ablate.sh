@@ -1,7 +1,10 @@
 #!/bin/bash
 # Timing-only ablations of the step kernel (results are NOT valid games).
+# Needs the ablation build (the product kernels compile the ablations out):
+#   make -C gym-simpletetris_amd/csrc variant V=ablation DEFS=-DST_ABLATION=1
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"; mkdir -p gpurun_out
+export ST_LIB="${ST_LIB:-$R/gym-simpletetris_amd/csrc/build/lib_ablation.so}"
 TAG=${TAG:-abl}
 for ab in 0 1 2 4 8 3 0; do
   ST_ABLATE=$ab timeout -k 10 120 python bench.py --steps 500 --warmup 50 --no-extras --no-cpu-baseline ${EXTRA} \
