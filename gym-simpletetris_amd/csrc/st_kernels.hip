@@ -349,10 +349,13 @@ __device__ __forceinline__ void mt_work(const MtRes &rs, bool want, uint32_t &mt
 }
 
 // Finish the next generation of ONE env (words [pg, 624)), wave-cooperatively
+// (out of line: inlined, its loop-invariant lane masks were hoisted into the
+// rollout's prologue and pushed its step loop past the SGPR limit -- spills
+// to VGPR lanes, reloaded every step; -5.5% packed rollout once out of line)
 // (wave-uniform arguments): the chunked recurrence in LDS -- [0,227) reads old
 // words | [227,454) reads [0,227) | [454,623) reads [227,396) | 623 reads 396
 // and 0, each chunk only words that are old or finished.
-__device__ void mt_finish(uint32_t *g, uint32_t *S, int lane, int pg, int cur) {
+__device__ __attribute__((noinline)) void mt_finish(uint32_t *g, uint32_t *S, int lane, int pg, int cur) {
     const uint32_t *src_new = g + (cur ? 0 : kMtB), *src_old = g + (cur ? kMtB : 0);
     uint32_t *dst = g + (cur ? 0 : kMtB);
     {
