@@ -943,8 +943,12 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
                                      ((uint32_t)e0 + (uint32_t)(4 * q) * (uint32_t)p.n + noff) * 4u, v);
                 }
             }
-        } else if (real) {
-            for (int x = 0; x < W; ++x) obs_t[x * p.n + e] = lcol(L, x, lane) & hmask;
+        } else if (real) {  // ragged / unaligned: one dword per row, 32-bit offsets (SGPRs)
+            const auto ro = buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u);
+#pragma unroll 1
+            for (int x = 0; x < W; ++x)
+                __builtin_amdgcn_raw_buffer_store_b32(lcol(L, x, lane) & hmask, ro,
+                                                      ((uint32_t)x * (uint32_t)p.n + (uint32_t)e) * 4u, 0, kNT);
         }
     }
     if (F32) {
