@@ -8,7 +8,7 @@ actions a[t, e] = splitmix64(seed ^ ((t << 32) ^ e)) % 7 that are generated
 into HBM before the timed region.  Envs auto-reset inside the
 step kernel when they die (reference driver `if done: env.reset()`).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c4] [--obs packed|f32]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c4] [--obs packed|f32] [--clear-heavy]
 
 N > 1 is launched by torch.distributed.run (one process per GPU, RCCL); each
 rank owns a contiguous block of global env indices and no collective runs in
@@ -125,6 +125,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="timed region only (profiling)")
+    ap.add_argument("--clear-heavy", action="store_true",
+                    help="also time st_step on a greedy-player (line-clearing) action stream; off by "
+                         "default so that the headline kernel's rocprofv3 average covers only the "
+                         "headline workload")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -254,7 +258,14 @@ def main():
     elapsed, ev_ms, p_lock = timed(run_main, K)
     value = n_global * K / elapsed
     event_ms = ev_ms / K
-    kname = f"k_step<10, 20, {'true' if f32 else 'false'}, false>"
+    sc0 = not cfg_kw  # no scoring flags: the SC0 specialization (st_kernels.hip launch_step)
+
+    def kname_of(kind, use_f32):  # rocprofv3's demangled name of the 10x20 kernel
+        b = lambda v: "true" if v else "false"  # noqa: E731
+        if kind == "step":
+            return f"k_step<10, 20, {b(use_f32)}, false, {b(sc0)}>"
+        return f"k_rollout<10, 20, {b(use_f32)}, {b(sc0)}>"
+    kname = kname_of("step", f32)
     out = {
         "metric": METRIC,
         "value": value,
@@ -299,7 +310,7 @@ def main():
             variants["step_f32"] = {
                 "value": n_global * K / el, "ms_per_step": el / K * 1e3, "p_lock": pl,
                 "roofline": roofline(ev / K, algorithmic_bytes(W, H, pl, True), 1,
-                                     "k_step<10, 20, true, false>")}
+                                     kname_of("step", True))}
             del g
         # K-step rollout kernel (st_rollout): CH steps per launch
         CH = min(args.rollout_chunk, K)
@@ -323,46 +334,51 @@ def main():
                 "value": n_global * nch * CH / el, "ms_per_step": el / (nch * CH) * 1e3,
                 "steps_per_launch": CH, "p_lock": pl,
                 "roofline": roofline(ev / nch, rollout_bytes(W, H, pl, use_f32, CH), CH,
-                                     f"k_rollout<10, 20, {'true' if use_f32 else 'false'}>")}
+                                     kname_of("rollout", use_f32))}
             del rf
-        # Clear-heavy regime: uniform actions almost never clear
-        # a line, so the same st_step is also timed on an action stream that
-        # a greedy placement player (st_policy_greedy, 3% random) produced from
-        # the same start state: recorded untimed, then replayed from a
-        # snapshot of that start state through the same hipGraph path.
-        ce = ShardedTetris(n_global, seed=1000, rank=rank, world=world, device=dev,
-                           autoreset="same_step", width=W, height=H, **cfg_kw).engine
-        ce.reset()
-        snap = ce.save()
-        gact = torch.empty((WU + K, n_local), dtype=torch.uint8, device=dev)
-        cleared = torch.zeros((), dtype=torch.int64, device=dev)
-        with torch.cuda.stream(s):
-            for t in range(WU + K):
-                ce.policy_greedy(t, seed=aseed, explore=30, out=gact[t])
-                C.check(L.st_step(ce._ctx, ctypes.c_void_p(gact[t].data_ptr()), p_obs, p_rew, p_done, sp))
-                if t >= WU:  # default rewards: +100 per cleared line
-                    cleared += rew_v.clamp(min=0).sum()
-        torch.cuda.synchronize(dev)
-        n_cleared = int(cleared.item())
-        ce.load(snap)
-        del snap
-        gptr = [ctypes.c_void_p(gact[t].data_ptr()) for t in range(WU + K)]
-        with torch.cuda.stream(s):
-            for t in range(WU):
-                C.check(L.st_step(ce._ctx, gptr[t], p_obs, p_rew, p_done, sp))
-        torch.cuda.synchronize(dev)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
-            for t in range(WU, WU + K):
-                C.check(L.st_step(ce._ctx, gptr[t], p_obs, p_rew, p_done, sp))
-        torch.cuda.synchronize(dev)
-        el, ev, _ = timed(g.replay, K)
-        variants["step_clear_heavy"] = {
-            "value": n_global * K / el, "ms_per_step": el / K * 1e3,
-            "lines_per_env_step": (n_cleared / 100.0 / (n_local * K)) if args.config == "c3" else None,
-            "actions": "st_policy_greedy (greedy placement, 3% uniform), recorded then replayed",
-            "kernel_us": ev / K * 1e3}
-        del g, ce
+
+        def clear_heavy(variants):
+            # Clear-heavy regime: uniform actions almost never clear
+            # a line, so the same st_step is also timed on an action stream that
+            # a greedy placement player (st_policy_greedy, 3% random) produced from
+            # the same start state: recorded untimed, then replayed from a
+            # snapshot of that start state through the same hipGraph path.
+            ce = ShardedTetris(n_global, seed=1000, rank=rank, world=world, device=dev,
+                               autoreset="same_step", width=W, height=H, **cfg_kw).engine
+            ce.reset()
+            snap = ce.save()
+            gact = torch.empty((WU + K, n_local), dtype=torch.uint8, device=dev)
+            cleared = torch.zeros((), dtype=torch.int64, device=dev)
+            with torch.cuda.stream(s):
+                for t in range(WU + K):
+                    ce.policy_greedy(t, seed=aseed, explore=30, out=gact[t])
+                    C.check(L.st_step(ce._ctx, ctypes.c_void_p(gact[t].data_ptr()), p_obs, p_rew, p_done, sp))
+                    if t >= WU:  # default rewards: +100 per cleared line
+                        cleared += rew_v.clamp(min=0).sum()
+            torch.cuda.synchronize(dev)
+            n_cleared = int(cleared.item())
+            ce.load(snap)
+            del snap
+            gptr = [ctypes.c_void_p(gact[t].data_ptr()) for t in range(WU + K)]
+            with torch.cuda.stream(s):
+                for t in range(WU):
+                    C.check(L.st_step(ce._ctx, gptr[t], p_obs, p_rew, p_done, sp))
+            torch.cuda.synchronize(dev)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                for t in range(WU, WU + K):
+                    C.check(L.st_step(ce._ctx, gptr[t], p_obs, p_rew, p_done, sp))
+            torch.cuda.synchronize(dev)
+            el, ev, _ = timed(g.replay, K)
+            variants["step_clear_heavy"] = {
+                "value": n_global * K / el, "ms_per_step": el / K * 1e3,
+                "lines_per_env_step": (n_cleared / 100.0 / (n_local * K)) if args.config == "c3" else None,
+                "actions": "st_policy_greedy (greedy placement, 3% uniform), recorded then replayed",
+                "kernel_us": ev / K * 1e3}
+            del g, ce
+
+        if args.clear_heavy:
+            clear_heavy(variants)
         out["variants"] = variants
         if args.gather and world > 1:
             torch.cuda.synchronize(dev)

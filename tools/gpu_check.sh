@@ -12,8 +12,10 @@ timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu_$T
  && echo "pytest ok" \
  && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 \
  && echo "smoke ok" \
- && timeout -k 10 600 python bench.py --steps 1000 --warmup 100 --cpu-seconds 10 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err \
- && echo "bench ok" && cat gpurun_out/bench_$TAG.json
+ && timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err \
+ && echo "bench ok" && cat gpurun_out/bench_$TAG.json \
+ && timeout -k 10 600 python bench.py --clear-heavy --no-cpu-baseline > gpurun_out/bench_clear_$TAG.json 2>> gpurun_out/bench_$TAG.err \
+ && echo "bench clear-heavy ok"
 
 
 rc=$?
