@@ -268,6 +268,28 @@ __device__ __forceinline__ void mt_unpack(uint32_t r, int &idx, int &pg, int &cu
 __device__ __forceinline__ uint32_t mt_pack(int idx, int pg, int cur) {
     return (uint32_t)idx | ((uint32_t)pg << 10) | ((uint32_t)cur << 20);
 }
+// The preview (the piece the env's NEXT spawn takes, drawn one spawn ahead so
+// that no step waits on a draw; see run_steps) in the upper bits of the same
+// word: pv << 21 | ok << 24 | c << 25, c = the MT words its draw consumed,
+// so the reference's state -- the one before the preview was drawn -- is c
+// words back (k_mt_sync).  ok = 0 (a host-written or synced state): the next
+// spawn draws its piece first, then the preview.
+constexpr uint32_t kMtLow = (1u << 21) - 1u;  // idx | pg | cur
+constexpr uint32_t kPvOk = 1u << 24;
+constexpr uint32_t kPvCMax = 127u;
+__device__ __forceinline__ uint32_t mt_keep(uint32_t hi, uint32_t low) { return (hi & ~kMtLow) | low; }
+__device__ __forceinline__ int pv_id(uint32_t r) { return (int)((r >> 21) & 7u); }
+__device__ __forceinline__ bool pv_ok(uint32_t r) { return (r & kPvOk) != 0u; }
+// words consumed between MT positions (idx0, cur0) and (idx1, cur1) (one
+// generation switch at most: a draw consumes > 624 words with p < 2^-600)
+__device__ __forceinline__ uint32_t mt_consumed(uint32_t before, uint32_t after) {
+    const int i0 = (int)(before & 0x3FFu), i1 = (int)(after & 0x3FFu);
+    const int c = ((before ^ after) >> 20) & 1u ? kMtN - i0 + i1 : i1 - i0;
+    return (uint32_t)c < kPvCMax ? (uint32_t)c : kPvCMax;
+}
+__device__ __forceinline__ uint32_t pv_pack(uint32_t mt_after, int pv, uint32_t c) {
+    return (mt_after & kMtLow) | ((uint32_t)pv << 21) | kPvOk | (c << 25);
+}
 
 // The wave's 64 MT states as one buffer resource.  Loads and stores of lanes
 // (or operands) not wanted get an out-of-range offset (loads read 0), so each
@@ -345,7 +367,7 @@ __device__ __forceinline__ void mt_work(const MtRes &rs, bool want, uint32_t &mt
     const uint32_t nb = cur ? 0u : kMtB;
     buf_store16<AUX>(rs.r, work ? rs.lane_off + 4u * (nb + (uint32_t)pg) : kOff, v);
     buf_store16<AUX>(rs.r, work && cur && pg < kMtWin ? rs.lane_off + 4u * (kMtPad + (uint32_t)pg) : kOff, v);
-    if (work) mtst = mt_pack(idx, pg + 4, cur);
+    if (work) mtst = mt_keep(mtst, mt_pack(idx, pg + 4, cur));
 }
 
 // Finish the next generation of ONE env (words [pg, 624)), wave-cooperatively
@@ -408,7 +430,9 @@ __device__ __attribute__((noinline)) void mt_finish(uint32_t *g, uint32_t *S, in
 // independent chains, each lane takes its first accepted one; lanes the
 // window does not settle (8 rejections, p <= 2^-8, or the generation's end)
 // continue in the loop, switching generations at index 624.
-template <int WIN>
+// COUNT: also count the drawn shape in cnt (a spawn's _new_piece :199; not
+// for a preview, which is counted when it spawns).
+template <int WIN, bool COUNT = true>
 __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t &mtst,
                                           uint32_t *mt_wave, uint32_t *S, int lane,
                                           const MtPre &pre, bool have_pre) {
@@ -498,7 +522,7 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
             }
         } while (__ballot(pending));
     }
-    if (need) mtst = mt_pack(idx, pg, cur);
+    if (need) mtst = mt_keep(mtst, mt_pack(idx, pg, cur));
     if (!need) return 0;
     int32_t rr = (int32_t)r + 1;
     int pick = 6;
@@ -511,8 +535,10 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
             found = true;
         }
     }
+    if constexpr (COUNT) {
 #pragma unroll
-    for (int i = 0; i < 7; ++i) cnt[i] += (i == pick);
+        for (int i = 0; i < 7; ++i) cnt[i] += (i == pick);
+    }
     return pick;
 }
 
@@ -532,16 +558,92 @@ __device__ __forceinline__ uint32_t pack_piece(int id, int rot, int ax, int ay, 
         }                                                              \
     } while (0)
 
-// One wave = 64 envs.  KSTEPS == 1: TetrisEngine.step once (st_step);
-// KSTEPS == 0: p.k consecutive steps (st_rollout) with the board and counters
-// kept in LDS between steps, actions read one step ahead, and per-step
-// outputs at [t].  State is loaded once at the start and stored once at the end.
+// LDS of the step kernels: one instance per workgroup, shared by its waves
+// (the two-wave st_step hands data between them through it).  Plain words
+// only (no vector-type members: a __shared__ object must be trivially
+// constructible).
+template <bool F32, int KSTEPS>
+struct StepLds {
+    // board columns L[x + kPad][lane], all-ones walls at both ends
+    uint32_t L[(kMaxW + 2 * kPad) * kWave] __attribute__((aligned(16)));
+    // staged counter rows SS[r][lane] (r < 14: stats rows, 14: piece word)
+    uint32_t SS[kHotQ * 4 * kWave] __attribute__((aligned(16)));
+    uint32_t T2[2 * 28] __attribute__((aligned(8)));  // piece table {m, g}
+    uint32_t S[kMtN];                                  // mt_finish scratch
+    // st_step: per env board keep-mask, changed board columns, changed
+    // counter rows of the logic (SD) and draw (SDD) waves
+    uint32_t KM[KSTEPS == 1 ? kWave : 4] __attribute__((aligned(16)));
+    uint32_t BD[KSTEPS == 1 ? kWave : 4] __attribute__((aligned(16)));
+    uint32_t SD[KSTEPS == 1 ? kWave : 4] __attribute__((aligned(16)));
+    uint32_t SDD[KSTEPS == 1 ? kWave : 4] __attribute__((aligned(16)));
+    // float32 obs writer (F32): per-lane obs words at stride W+1 (conflict-
+    // free transposed reads) and the 16 float4 patterns of a 4-bit nibble
+    uint32_t O[F32 ? kWave * (kMaxW + 1) : 1];
+    float F4[F32 ? 64 : 4] __attribute__((aligned(16)));
+    // two-wave st_step hand-offs (see run_steps)
+    uint32_t dump[kWave] __attribute__((aligned(16)));  // the logic wave's padding-row writes
+    // (step-parity double buffers where a wave may write step t+1's value
+    // before the other has read step t's)
+    uint32_t lockm[2][2], drawm[2];
+    uint32_t pick1[kWave];
+    uint32_t mtw[2][KSTEPS == 1 ? 1 : kWave];  // rollouts: the draw wave's MT word after step t
+    uint32_t f1, f2;  // = t + 1 once step t's draw mask / first picks are written
+};
+
+// Roles of run_steps.  st_step runs TWO waves per 64 envs: the logic wave
+// (action, lock path, board / obs / counter outputs) and the draw wave (MT
+// words, the next-generation block, the piece draw), so the draw no longer
+// sits on the logic wave's chain.  That works because spawns take a piece
+// drawn one spawn AHEAD (the "preview", kept in the MT state word): a spawn
+// needs no draw result from the same step, and the draw wave's draw -- the
+// next preview -- is only stored.  The reference's RNG sequence is unchanged
+// (every spawn / reset still consumes the next draw, with the shape counts of
+// that moment: the preview is drawn right after the previous spawn's count
+// update, and counts change only at spawns); st_mt_sync rewinds the preview's
+// words for the host.  Rollouts run both roles in one wave (kRoleOne).
+constexpr int kRoleOne = 0;
+constexpr int kRoleL = 1;
+constexpr int kRoleD = 2;
+
+__device__ __forceinline__ void wg_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+// One-way LDS hand-off between the two waves of a workgroup without a
+// barrier (the writer must not wait for the reader).  A wave's LDS accesses
+// execute in order, so data it wrote before the flag are visible to a wave
+// that has seen the flag; the asm statements only keep the compiler from
+// moving LDS accesses across the hand-off (no s_waitcnt: the writer's
+// outstanding global stores are not drained).
+// (LDS address space explicitly: through a generic pointer the accesses
+// become flat_* instructions, which count in vmcnt and wait for it.)
+typedef __attribute__((address_space(3))) volatile uint32_t lds_vu32;
+__device__ __forceinline__ void lds_flag_set(uint32_t *f, uint32_t v) {
+    asm volatile("" ::: "memory");
+    *(lds_vu32 *)f = v;
+    asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void lds_flag_wait(uint32_t *f, uint32_t v) {
+    asm volatile("" ::: "memory");
+    while (*(lds_vu32 *)f != v) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+
+// KSTEPS == 1: TetrisEngine.step once (st_step), ROLE = kRoleL / kRoleD (the
+// two waves of a workgroup) or kRoleOne; KSTEPS == 0: p.k consecutive steps
+// (st_rollout, kRoleOne) with the board and counters kept in LDS between
+// steps, actions read one step ahead, and per-step outputs at [t].  State is
+// loaded once at the start and stored once at the end.
 // SC0: the context has no scoring flags (the reference's defaults,
 // tetris_env.py:126-137): those tests fold away at compile time (measured:
 // the rollout loop otherwise holds each flag as a 64-bit lane mask at the
 // SGPR limit, -5% packed rollout; st_step -1%).
-template <int WT, int HT, bool F32, bool STAMP, int KSTEPS, bool SC0 = false>
-__device__ __forceinline__ void run_steps(const KParams &p) {
+template <int WT, int HT, bool F32, bool STAMP, int KSTEPS, bool SC0, int ROLE>
+__device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS> &sm) {
+    constexpr bool DO_L = ROLE != kRoleD;  // action, lock path, outputs
+    constexpr bool DO_D = ROLE != kRoleL;  // MT words, next-generation block, draws
+    constexpr bool TWO = ROLE != kRoleOne;
     [[maybe_unused]] uint64_t tstamp[10] = {};
     [[maybe_unused]] uint64_t draw_kind = 0;  // stamp build: 1 = a lane twisted, 2 = a draw ran past 8 words
     constexpr bool S32 = HT != 0 && HT <= 25;  // see pc_bits
@@ -558,24 +660,11 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     [[maybe_unused]] uint64_t rt0 = 0;
     if constexpr (STAMP) rt0 = __builtin_amdgcn_s_memrealtime();
     ST_STAMP(0);
-    // LDS: board columns L[x + kPad][lane] (walls at both ends), the staged
-    // counter rows SS[r][lane] (r < 14: stats rows, 14: piece word), the
-    // piece table and the MT scratch of mt_finish.
-    __shared__ __attribute__((aligned(16))) uint32_t L[(kMaxW + 2 * kPad) * kWave];
-    __shared__ __attribute__((aligned(16))) uint32_t SS[kHotQ * 4 * kWave];
-    __shared__ uint2 T2[28];
-    __shared__ uint32_t S[kMtN];
-    // st_step: per env board keep-mask, changed board columns, changed counter rows
-    __shared__ __attribute__((aligned(16))) uint32_t KM[KSTEPS == 1 ? kWave : 4];
-    __shared__ __attribute__((aligned(16))) uint32_t BD[KSTEPS == 1 ? kWave : 4];
-    __shared__ __attribute__((aligned(16))) uint32_t SD[KSTEPS == 1 ? kWave : 4];
-    // float32 obs writer (F32): per-lane obs words at stride W+1 (conflict-
-    // free transposed reads) and the 16 float4 patterns of a 4-bit nibble.
-    __shared__ uint32_t O[F32 ? kWave * (kMaxW + 1) : 1];
-    __shared__ __attribute__((aligned(16))) float4 F4[F32 ? 16 : 1];
+    uint32_t *const L = sm.L;
+    uint32_t *const SS = sm.SS;
     const int W = WT ? WT : p.W;
     const int H = HT ? HT : p.H;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & (kWave - 1);
     const int64_t e0 = (int64_t)blockIdx.x * kWave;
     const int64_t e = e0 + lane;
     const int64_t sd = p.stride;
@@ -589,10 +678,13 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     // addresses are SGPR base + VGPR offset.  The board allocation is padded
     // to a multiple of 4 rows; rows >= W land in the right-wall LDS columns,
     // which are written after them.  Counter rows: 0..14 plus row 15 (unused).
+    // Two waves: the logic wave loads the board and counter groups 0-1
+    // (time .. count1), the draw wave groups 2-3 (count2 .. MT word, piece).
     const uint32_t loff = (uint32_t)(lane >> 4) * (uint32_t)sd + 4u * (uint32_t)(lane & 15);
     constexpr int NBQ = ((WT ? WT : kMaxW) + 3) / 4;  // board 4-row groups
     const uint32_t *bsrc = p.board + e0;
     const uint32_t *ssrc = reinterpret_cast<const uint32_t *>(p.stats) + e0;
+    auto mine_q = [&](int q) { return ROLE == kRoleOne || (ROLE == kRoleL) == (q < 2); };
     // Rows past the last real row (board padding, counter row 15) re-read the
     // last row -- the same cache line another lane fetches -- instead of
     // fetching padding; the loads stay unconditional (a load under a branch
@@ -602,64 +694,99 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
         return (uint32_t)r * (uint32_t)sd + 4u * (uint32_t)(lane & 15);
     };
     uint4 bv[NBQ];
+    if constexpr (DO_L) {
 #pragma unroll
-    for (int q = 0; q < NBQ; ++q)
-        if (WT || 4 * q < W)
-            bv[q] = *reinterpret_cast<const uint4 *>(bsrc + (size_t)(4 * q) * sd +
-                                                     (4 * q + 4 <= W ? loff : clamp_off(q, W)));
+        for (int q = 0; q < NBQ; ++q)
+            if (WT || 4 * q < W)
+                bv[q] = *reinterpret_cast<const uint4 *>(bsrc + (size_t)(4 * q) * sd +
+                                                         (4 * q + 4 <= W ? loff : clamp_off(q, W)));
+    }
     uint4 sv[kHotQ];
 #pragma unroll
     for (int q = 0; q < kHotQ; ++q)
-        sv[q] = *reinterpret_cast<const uint4 *>(ssrc + (size_t)(4 * q) * sd +
-                                                 (4 * q + 4 <= kHotRows ? loff : clamp_off(q, kHotRows)));
+        if (mine_q(q))
+            sv[q] = *reinterpret_cast<const uint4 *>(ssrc + (size_t)(4 * q) * sd +
+                                                     (4 * q + 4 <= kHotRows ? loff : clamp_off(q, kHotRows)));
     const int K = KSTEPS ? KSTEPS : p.k;
     // unconditional (clamped) so it is issued with the others; masked at use
-    uint32_t act_next = p.actions[real ? e : p.n - 1];
+    uint32_t act_next = 0;
+    if constexpr (DO_L) act_next = p.actions[real ? e : p.n - 1];
     // The piece table, lane i = entry i, from immediates by compare/select
     // (VALU under the load latency; no memory access: a __constant__ load
     // gets sunk by the compiler past the state loads' completion -- one more
     // serialized round trip -- and inline asm here makes the register
-    // allocator spill the in-flight state loads to scratch).
+    // allocator spill the in-flight state loads to scratch).  Two waves: the
+    // draw wave builds it (and the walls, and the f32 nibble table).
+    constexpr bool BUILD = ROLE != kRoleL;
     uint32_t tab_m = 0, tab_g = 0;
+    if constexpr (BUILD) {
 #pragma unroll
-    for (int i = 0; i < 28; ++i) {
-        const bool me = lane == i;
-        tab_m = me ? kTab.m[i] : tab_m;
-        tab_g = me ? kTab.g[i] : tab_g;
+        for (int i = 0; i < 28; ++i) {
+            const bool me = lane == i;
+            tab_m = me ? kTab.m[i] : tab_m;
+            tab_g = me ? kTab.g[i] : tab_g;
+        }
     }
-    const uint32_t floor_op = floorb;
     const int lrow = lane >> 4, lcc = 4 * (lane & 15);  // this lane's row-in-group, env slot
+    if constexpr (DO_L) {
 #pragma unroll
-    for (int q = 0; q < NBQ; ++q) {
-        if (WT || 4 * q < W) {
-            uint4 v = bv[q];
-            v.x |= floor_op;
-            v.y |= floor_op;
-            v.z |= floor_op;
-            v.w |= floor_op;
-            *reinterpret_cast<uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]) = v;
+        for (int q = 0; q < NBQ; ++q) {
+            // rows >= W (allocation padding) land in the right-wall columns:
+            // one wave writes them first and the walls over them; the logic
+            // wave of two sends them to a dump slot (the draw wave writes the
+            // walls) -- an address select, not a branch: a store under a
+            // branch gets its load sunk into the branch, one more round trip
+            if (WT || 4 * q < W) {
+                uint4 v = bv[q];
+                v.x |= floorb;
+                v.y |= floorb;
+                v.z |= floorb;
+                v.w |= floorb;
+                uint32_t *dst = &L[(4 * q + lrow + kPad) * kWave + lcc];
+                if constexpr (ROLE == kRoleL) dst = 4 * q + lrow < W ? dst : &sm.dump[lcc];
+                *reinterpret_cast<uint4 *>(dst) = v;
+            }
+        }
+    }
+    if constexpr (BUILD) {
+#pragma unroll
+        for (int x = 0; x < kPad; ++x) {
+            L[x * kWave + lane] = ~0u;
+            L[(W + kPad + x) * kWave + lane] = ~0u;
+        }
+        if (lane < 28) {
+            sm.T2[2 * lane] = tab_m;
+            sm.T2[2 * lane + 1] = tab_g;
+        }
+        if constexpr (F32) {
+            if (lane < 16) {
+                sm.F4[4 * lane] = (float)(lane & 1);
+                sm.F4[4 * lane + 1] = (float)((lane >> 1) & 1);
+                sm.F4[4 * lane + 2] = (float)((lane >> 2) & 1);
+                sm.F4[4 * lane + 3] = (float)((lane >> 3) & 1);
+            }
         }
     }
 #pragma unroll
-    for (int x = 0; x < kPad; ++x) {  // walls (after the board slots, see above)
-        L[x * kWave + lane] = ~0u;
-        L[(W + kPad + x) * kWave + lane] = ~0u;
-    }
-#pragma unroll
     for (int q = 0; q < kHotQ; ++q)
-        *reinterpret_cast<uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]) = sv[q];
-    if (lane < 28) T2[lane] = make_uint2(tab_m, tab_g);
-    if constexpr (F32) {
-        if (lane < 16)
-            F4[lane] = make_float4((float)(lane & 1), (float)((lane >> 1) & 1),
-                                   (float)((lane >> 2) & 1), (float)((lane >> 3) & 1));
+        if (mine_q(q)) *reinterpret_cast<uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]) = sv[q];
+    if constexpr (TWO) {
+        if (ROLE == kRoleL && lane == 0) sm.f1 = 0u;
+        if (ROLE == kRoleD && lane == 0) sm.f2 = 0u;
+        wg_barrier();  // B0: the staged state is complete
+    } else {
+        wave_sync();
     }
-    wave_sync();
     auto ss = [&](int r) -> uint32_t & { return SS[r * kWave + lane]; };
+    auto tab = [&](int i) -> uint2 { return *reinterpret_cast<const uint2 *>(&sm.T2[2 * i]); };
 
     for (int t = 0; t < K; ++t) {
-    const uint32_t act = real ? act_next : 6u;
-    if (KSTEPS != 1 && t + 1 < K) act_next = p.actions[(int64_t)(t + 1) * p.n + (real ? e : p.n - 1)];
+    // ---------------- logic: action, gravity, lock decision ----------------
+    uint32_t act = 6u;
+    if constexpr (DO_L) {
+        act = real ? act_next : 6u;
+        if (KSTEPS != 1 && t + 1 < K) act_next = p.actions[(int64_t)(t + 1) * p.n + (real ? e : p.n - 1)];
+    }
     uint32_t *const obs_t = p.obs ? p.obs + (int64_t)t * W * p.n : nullptr;
     const uint32_t pw = ss(kPieceRow);
     int32_t time = (int32_t)ss(ST_STAT_TIME);
@@ -668,67 +795,98 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     int ax = (int)((pw >> 5) & 63u);
     int ay = (int)((pw >> 11) & 63u);
     int lock = (int)(pw >> 17);
+    // MT word at the start of the step (the logic wave uses only the preview
+    // bits; in a two-wave step the draw wave replaces the row after B1, and in
+    // a two-wave rollout it hands step t-1's word over in mtw: read after B1)
+    uint32_t mt0 = ss(ST_STAT_MT_INDEX);
     if constexpr (STAMP) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     ST_STAMP(1);
 
-    // ---- action (tetris_env.py:245; value_action_map :152-160) + drop ----
-    // Current and candidate descriptors and their columns are read in one
-    // LDS round trip each; the collision and drop tests are then pure VALU.
-    const bool tries = act == 0u || act == 1u || act == 4u || act == 5u;
-    const int cx = ax + (act == 0u ? -1 : (act == 1u ? 1 : 0));
-    const int cr = act == 4u ? ((rot + 1) & 3) : (act == 5u ? ((rot + 3) & 3) : rot);
-    uint2 desc = T2[id * 4 + rot];
-    const uint2 cdesc = T2[id * 4 + cr];
-    uint32_t cur[4], cand[4];
-    read_cols(L, lane, desc.y, ax, cur);
-    read_cols(L, lane, cdesc.y, cx, cand);
-    // branch-free: select the accepted position's descriptor and columns, then
-    // one drop test (both arms would otherwise run in a divergent wave)
-    const bool ok = tries && !collides_v<S32>(cdesc.x, ay, cand);
-    ax = ok ? cx : ax;
-    rot = ok ? cr : rot;
-    desc.x = ok ? cdesc.x : desc.x;
-    desc.y = ok ? cdesc.y : desc.y;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) cur[j] = ok ? cand[j] : cur[j];
-    int d = drop_v(desc.y, ay, cur);
-    if (act == 2u) {                 // hard_drop :54-59
-        ay += d;
-        d = 0;
-    } else if (act == 3u && d > 0) { // soft_drop :49-51
-        ay += 1;
-        d -= 1;
-    }
-    // ---- gravity + lock delay (tetris_env.py:247-262) ----
-    if (d > 0) {
-        ay += 1;
-        d -= 1;
-        if (kFlags & ST_STEP_RESET) lock = 0;
-    }
-    time += 1;
-    int32_t rew = (kFlags & ST_REWARD_STEP) ? 1 : 0;
+    uint2 desc = make_uint2(0u, 0u);
     bool locknow = false;
-    if (d == 0) {
-        const int l1 = lock + 1;  // (x + 1) % lock_mod; x < lock_mod unless set_state said otherwise
-        lock = l1 < p.lock_mod ? l1 : (l1 == p.lock_mod ? 0 : l1 % p.lock_mod);
-        locknow = lock == 0 && !(kAblate & 1u);
+    int32_t rew = 0;
+    if constexpr (DO_L) {
+        // ---- action (tetris_env.py:245; value_action_map :152-160) + drop ----
+        // Current and candidate descriptors and their columns are read in one
+        // LDS round trip each; the collision and drop tests are then pure VALU.
+        const bool tries = act == 0u || act == 1u || act == 4u || act == 5u;
+        const int cx = ax + (act == 0u ? -1 : (act == 1u ? 1 : 0));
+        const int cr = act == 4u ? ((rot + 1) & 3) : (act == 5u ? ((rot + 3) & 3) : rot);
+        desc = tab(id * 4 + rot);
+        const uint2 cdesc = tab(id * 4 + cr);
+        uint32_t cur[4], cand[4];
+        read_cols(L, lane, desc.y, ax, cur);
+        read_cols(L, lane, cdesc.y, cx, cand);
+        // branch-free: select the accepted position's descriptor and columns, then
+        // one drop test (both arms would otherwise run in a divergent wave)
+        const bool ok = tries && !collides_v<S32>(cdesc.x, ay, cand);
+        ax = ok ? cx : ax;
+        rot = ok ? cr : rot;
+        desc.x = ok ? cdesc.x : desc.x;
+        desc.y = ok ? cdesc.y : desc.y;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cur[j] = ok ? cand[j] : cur[j];
+        int d = drop_v(desc.y, ay, cur);
+        if (act == 2u) {                 // hard_drop :54-59
+            ay += d;
+            d = 0;
+        } else if (act == 3u && d > 0) { // soft_drop :49-51
+            ay += 1;
+            d -= 1;
+        }
+        // ---- gravity + lock delay (tetris_env.py:247-262) ----
+        if (d > 0) {
+            ay += 1;
+            d -= 1;
+            if (kFlags & ST_STEP_RESET) lock = 0;
+        }
+        time += 1;
+        rew = (kFlags & ST_REWARD_STEP) ? 1 : 0;
+        if (d == 0) {
+            const int l1 = lock + 1;  // (x + 1) % lock_mod; x < lock_mod unless set_state said otherwise
+            lock = l1 < p.lock_mod ? l1 : (l1 == p.lock_mod ? 0 : l1 % p.lock_mod);
+            locknow = lock == 0 && !(kAblate & 1u);
+        }
     }
     ST_STAMP(2);
-    // MT window for the piece this lock will draw: issued now, consumed after
-    // the lock path (every locking lane draws: a spawn, or the same-step
-    // reset's), and the operands of its next-generation block (mt_work).
-    uint32_t mtst = ss(ST_STAT_MT_INDEX);  // packed (mt_pack)
-    const bool want_pre = locknow && !(kAblate & 2u);
-    const MtRes mrs = mt_res(p.mt + e0 * kMtPitch, lane);
-    MtPre pre;
-    constexpr int kWin = KSTEPS == 1 ? 16 : 8;
-    mt_pre_load<kWin>(mrs, mtst, want_pre, pre);
+    if constexpr (TWO) {
+        if constexpr (DO_L) {
+            const uint64_t m = __ballot(locknow);
+            if (lane == 0) {
+                sm.lockm[t & 1][0] = (uint32_t)m;
+                sm.lockm[t & 1][1] = (uint32_t)(m >> 32);
+            }
+        }
+        wg_barrier();  // B1: the draw wave learns which lanes lock
+        if constexpr (DO_D) {
+            const uint32_t w = lane < 32 ? sm.lockm[t & 1][0] : sm.lockm[t & 1][1];
+            locknow = (w >> (lane & 31)) & 1u;
+        }
+        if constexpr (DO_L && KSTEPS != 1) {
+            if (t > 0) mt0 = sm.mtw[(t - 1) & 1][lane];
+        }
+    }
 
-    // ---- lock path (tetris_env.py:263-299) ----
+    // ---------------- draw: MT window + block operands, issued now ----------------
+    // Every locking lane draws (its next preview, or -- without a valid
+    // preview -- its piece first) and builds one block of its next generation
+    // (mt_work); the words are consumed after the lock path in one wave, or
+    // right away by the draw wave.
+    uint32_t mtst = mt0;  // packed (mt_pack + preview bits)
+    const bool want_pre = locknow && !(kAblate & 2u);
+    constexpr int kWin = KSTEPS == 1 || TWO ? 16 : 8;
+    MtPre pre;
+    [[maybe_unused]] MtRes mrs;
+    if constexpr (DO_D) {
+        mrs = mt_res(p.mt + e0 * kMtPitch, lane);
+        mt_pre_load<kWin>(mrs, mtst, want_pre, pre);
+    }
+
+    // ---------------- logic: lock path (tetris_env.py:263-299) ----------------
     bool died = false, spawn = false;
     int32_t score = 0, lines = 0, holes = 0, height = 0, deaths = 0;
     uint32_t bdirty = 0;  // st_step: board columns this step changes (stores skip the rest)
-    if (locknow) {
+    if (DO_L && locknow) {
         score = (int32_t)ss(ST_STAT_SCORE);
         lines = (int32_t)ss(ST_STAT_LINES);
         holes = (int32_t)ss(ST_STAT_HOLES);
@@ -807,34 +965,47 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     ST_STAMP(3);
 
     const bool reset_now = died && p.autoreset == ST_AUTORESET_SAME_STEP;
-    const bool draw = spawn || reset_now;
-    // reward / done never depend on the piece drawn below.  Buffer stores
-    // (buf_rsrc): vmcnt counts loads and stores in issue order, and a store
-    // skipped on some path would make the MT-word wait in the draw vmcnt(0).
-    auto store_rd = [&]() {
+    // a lock consumes the preview (spawn, or the same-step reset's new piece);
+    // a death without auto-reset does not (the next st_reset takes it)
+    bool draw = spawn || reset_now;
+    if constexpr (TWO) {
+        if (DO_L && p.autoreset != ST_AUTORESET_SAME_STEP) {
+            const uint64_t m = __ballot(draw);
+            if (lane == 0) {
+                sm.drawm[0] = (uint32_t)m;
+                sm.drawm[1] = (uint32_t)(m >> 32);
+                lds_flag_set(&sm.f1, (uint32_t)t + 1u);
+            }
+        }
+    }
+    uint2 odesc = desc;
+    int oax = ax, oay = ay;
+    if constexpr (DO_L) {
+        // reward / done never depend on the piece drawn below.  Buffer stores
+        // (buf_rsrc): vmcnt counts loads and stores in issue order, and a store
+        // skipped on some path would make a later load's wait vmcnt(0).
         const auto rr = buf_rsrc(p.reward ? p.reward + (int64_t)t * p.n : nullptr, (uint32_t)p.n * 4u);
         const auto rd = buf_rsrc(p.done ? p.done + (int64_t)t * p.n : nullptr, (uint32_t)p.n);
         __builtin_amdgcn_raw_buffer_store_b32(rew, rr, real ? (uint32_t)e * 4u : kOff, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b8((char)(died ? 1 : 0), rd, real ? (uint32_t)e : kOff, 0, 0);
-    };
-    store_rd();
-    if constexpr (KSTEPS == 1) {
-        // The post-step board never depends on the drawn piece either (a spawn
-        // only overlays row 0, which is empty after a non-fatal lock, :277), so
-        // st_step stores it here and the stores drain under the MT-word wait:
-        // non-locking lanes and spawns: L; a death without auto-reset: L minus
-        // the locked piece (R8: _set_piece(False), :303); a same-step reset:
-        // the empty board.  The obs overlay of every non-spawning lane is then
-        // painted (a death's terminal obs = L with its piece, :301).
+    }
+    if constexpr (DO_L && KSTEPS == 1) {
+        // The post-step board never depends on the spawned piece either (a
+        // spawn only overlays row 0, which is empty after a non-fatal lock,
+        // :277), so st_step stores it here: non-locking lanes and spawns: L; a
+        // death without auto-reset: L minus the locked piece (R8:
+        // _set_piece(False), :303); a same-step reset: the empty board.  The
+        // obs overlay of every non-spawning lane is then painted (a death's
+        // terminal obs = L with its piece, :301).
         // Only rows (board columns x) that one of the lane's 4 envs changed are
         // written (buffer stores, see buf_rsrc).
         if (died && !reset_now) erase<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
         if (died) bdirty = ~0u;
-        KM[lane] = reset_now ? 0u : hmask;
-        BD[lane] = bdirty;
+        sm.KM[lane] = reset_now ? 0u : hmask;
+        sm.BD[lane] = bdirty;
         wave_sync();
-        const uint4 km = *reinterpret_cast<const uint4 *>(&KM[lcc]);
-        const uint4 bd4 = *reinterpret_cast<const uint4 *>(&BD[lcc]);
+        const uint4 km = *reinterpret_cast<const uint4 *>(&sm.KM[lcc]);
+        const uint4 bd4 = *reinterpret_cast<const uint4 *>(&sm.BD[lcc]);
         const uint32_t bdl = (bd4.x | bd4.y | bd4.z | bd4.w) >> lrow;
         uint4 bw[NBQ];
 #pragma unroll
@@ -861,157 +1032,214 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     }
 
     ST_STAMP(8);  // (stamp 8: between the early stores and the draw)
-    // ---- spawn (:299 _new_piece) or same-step reset (:306-315) ----
-    int32_t cnt[7];
+    // ---------------- draw (tetris_env.py:183-199, :299 _new_piece, :306-315 clear) ----------------
+    // spawn id: the preview; lanes without one draw their piece first
+    int sid = pv_id(mt0);
+    if constexpr (DO_D) {
+        // speculative in the draw wave (it does not know yet which locking
+        // lanes die without auto-reset): committed below only where `draw`
+        const bool dr_spec = TWO ? locknow : draw;
+        int32_t cnt[7];
 #pragma unroll
-    for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)ss(ST_STAT_COUNT0 + i);  // used by drawing lanes only
-    int pick = 0;
-    [[maybe_unused]] const uint32_t mt_before = mtst;
-    if constexpr (STAMP) {  // diagnostic split of the draw: MT-word wait | compute
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        ST_STAMP(9);
-    }
-    if (!(kAblate & 2u)) {
-        mt_pre_consume<kWin>(pre);
-        mt_work<KSTEPS == 1 ? kNT : 0>(mrs, want_pre, mtst, pre);  // before the draw: a switch it makes resets the progress
-        pick = draw_shape<kWin>(draw, cnt, mtst, p.mt + e0 * kMtPitch, S, lane, pre, want_pre);
-    }
-    ST_STAMP(4);
-    if constexpr (STAMP) {  // 1: a draw started a generation, 2: a draw ran past its 8 words
-        const int i0 = (int)(mt_before & 0x3FFu), i1 = (int)(mtst & 0x3FFu);
-        draw_kind = (__ballot(draw && i1 < i0) ? 1u : 0u) | (__ballot(draw && i1 >= i0 && i1 - i0 > 8) ? 2u : 0u);
-    }
-    uint2 odesc = desc;
-    int oax = ax, oay = ay;
-    uint32_t pw_out = pack_piece(id, rot, ax, ay, lock);
-    if (draw) pw_out = pack_piece(pick, 0, W / 2, 0, lock);
-    if (spawn) {
-        odesc = T2[pick * 4];
-        oax = W / 2;
-        oay = 0;
-    }
-
-    // ---- counters back to the staged rows (tetris_env.py:253, :264-299) ----
-    if (reset_now) {  // the finished episode's counters (ST_AUTORESET_SAME_STEP)
-        int32_t *st = p.stats + e;
-        st[ST_STAT_EP_TIME * sd] = time;
-        st[ST_STAT_EP_SCORE * sd] = score;
-        st[ST_STAT_EP_LINES * sd] = lines;
-        st[ST_STAT_EP_HOLES * sd] = holes;
-        time = score = lines = holes = height = 0;
-    }
-    // st_step stores only the counter rows that changed (sdirty, per env)
-    [[maybe_unused]] uint32_t sdirty = (1u << ST_STAT_TIME) | (1u << kPieceRow);
-    ss(ST_STAT_TIME) = (uint32_t)time;
-    ss(kPieceRow) = pw_out;
-    if (locknow) {
-        auto put = [&](int r, int32_t v) {
-            if constexpr (KSTEPS == 1) sdirty |= (uint32_t)(ss(r) != (uint32_t)v) << r;
-            ss(r) = (uint32_t)v;
-        };
-        put(ST_STAT_SCORE, score);
-        put(ST_STAT_LINES, lines);
-        put(ST_STAT_HOLES, holes);
-        put(ST_STAT_PIECE_HEIGHT, height);
-        put(ST_STAT_DEATHS, deaths);
-        put(ST_STAT_MT_INDEX, (int32_t)mtst);
-        if (draw) {
-            atomicAdd(&ss(ST_STAT_COUNT0 + pick), 1u);  // shape_counts[name] += 1, :199 (ds_add, no return)
-            sdirty |= 1u << (ST_STAT_COUNT0 + pick);
+        for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)ss(ST_STAT_COUNT0 + i);  // used by drawing lanes only
+        if constexpr (STAMP) {  // diagnostic split of the draw: MT-word wait | compute
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            ST_STAMP(9);
         }
-    }
-    if constexpr (KSTEPS == 1) SD[lane] = sdirty;
-
-    // ---- observation (tetris_env.py:301-302): board + current piece ----
-    if (KSTEPS != 1 || spawn) paint<S32>(L, lane, odesc.x, odesc.y, oax, oay, hmask);
-    wave_sync();
-    const bool wide_obs = (p.n & 3) == 0 && e0 + kWave <= p.n &&
-                          (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0;
-    if (obs_t && !(kAblate & 8u)) {
-        if (wide_obs) {
-            const uint32_t noff = (uint32_t)lrow * (uint32_t)p.n + (uint32_t)lcc;
-#pragma unroll
-            for (int q = 0; q < NBQ; ++q) {  // interleaved read/store (measured: reads-first
-                                             // costs the packed rollout ~7%)
-                if ((WT || 4 * q < W) && 4 * q + lrow < W) {
-                    uint4 v = *reinterpret_cast<const uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]);
-                    v.x &= hmask;
-                    v.y &= hmask;
-                    v.z &= hmask;
-                    v.w &= hmask;
-                    buf_store16<kNT>(buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u),
-                                     ((uint32_t)e0 + (uint32_t)(4 * q) * (uint32_t)p.n + noff) * 4u, v);
-                }
+        [[maybe_unused]] const uint32_t mt_before = mtst;
+        uint32_t mt_new = mtst;
+        if (!(kAblate & 2u)) {
+            mt_pre_consume<kWin>(pre);
+            mt_work<KSTEPS == 1 ? kNT : 0>(mrs, want_pre, mtst, pre);  // before the draws: a switch resets the progress
+            const bool need1 = dr_spec && !pv_ok(mt0);
+            if (__ballot(need1)) {  // rare: after st_seed / st_mt_sync / a host-written state
+                const int pk = draw_shape<kWin, false>(need1, cnt, mtst, p.mt + e0 * kMtPitch, sm.S, lane, pre, false);
+                if (need1) sid = pk;
             }
-        } else if (real) {  // ragged / unaligned: one dword per row, 32-bit offsets (SGPRs)
-            const auto ro = buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u);
-#pragma unroll 1
-            for (int x = 0; x < W; ++x)
-                __builtin_amdgcn_raw_buffer_store_b32(lcol(L, x, lane) & hmask, ro,
-                                                      ((uint32_t)x * (uint32_t)p.n + (uint32_t)e) * 4u, 0, kNT);
+            if constexpr (TWO) {
+                sm.pick1[lane] = (uint32_t)sid;
+                if (lane == 0) lds_flag_set(&sm.f2, (uint32_t)t + 1u);
+            }
+#pragma unroll
+            for (int i = 0; i < 7; ++i) cnt[i] += (dr_spec && i == sid);  // _new_piece :199
+            const uint32_t m0 = mtst;
+            const int npv = draw_shape<kWin, false>(dr_spec, cnt, mtst, p.mt + e0 * kMtPitch, sm.S, lane, pre,
+                                                     want_pre && pv_ok(mt0));
+            mt_new = pv_pack(mtst, npv, mt_consumed(m0, mtst));
+        } else if constexpr (TWO) {
+            sm.pick1[lane] = (uint32_t)sid;
+            if (lane == 0) lds_flag_set(&sm.f2, (uint32_t)t + 1u);
         }
-    }
-    if (F32) {
-        // float32 obs [n][W][H] of the wave's envs is one contiguous block,
-        // written as lane-consecutive float4 chunks.
-        const int64_t nreal64 = p.n - e0 < kWave ? p.n - e0 : kWave;
-        const int nreal = (int)nreal64;
-        float *out = p.obs_f32 + ((int64_t)t * p.n + e0) * (W * H);
-        if constexpr (WT != 0 && HT % 4 == 0) {
-            // chunk c = (env, column x, nibble q): 4 floats = bits 4q..4q+3 of
-            // the column word; the float4 comes from the 16-entry table.
-            constexpr int CPC = HT / 4, CPE = WT * CPC;
-#pragma unroll
-            for (int x = 0; x < WT; ++x) O[lane * (WT + 1) + x] = lcol(L, x, lane) & hmask;
-            wave_sync();
-            float4 *out4 = reinterpret_cast<float4 *>(out);
-            const int total = nreal * CPE;
-            for (int c = lane; c < total; c += kWave) {
-                const int ee = c / CPE;
-                const int cr = c - ee * CPE;
-                const int x = cr / CPC;
-                const int q = cr - x * CPC;
-                const float4 f = F4[(O[ee * (WT + 1) + x] >> (4 * q)) & 15u];
-                if constexpr (KSTEPS != 1) {
-                    // rollouts: non-temporal (A/B: -13% f32 rollout; the MT and
-                    // state lines stay in L2 instead of the streamed obs; +7% on
-                    // the single-step launch before its other stores were
-                    // made nt, +-0 after, so it keeps plain stores)
-                    typedef float f32x4 __attribute__((ext_vector_type(4)));
-                    const f32x4 fv = {f.x, f.y, f.z, f.w};
-                    __builtin_nontemporal_store(fv, reinterpret_cast<f32x4 *>(&out4[c]));
-                } else {
-                    out4[c] = f;
-                }
-            }
-        } else {
-            const int per_env = W * H;
-            const int total = nreal * per_env;
-            auto word = [&](int ee, int x) { return L[(x + kPad) * kWave + ee] & hmask; };
-            for (int f = lane; f < total; f += kWave) {
-                const int ee = f / per_env;
-                const int rem = f - ee * per_env;
-                const int x = rem / H;
-                const int y = rem - x * H;
-                out[f] = (float)((word(ee, x) >> y) & 1u);
+        ST_STAMP(4);
+        if constexpr (STAMP) {  // 1: a draw started a generation, 2: a draw ran past its 8 words
+            const int i0 = (int)(mt_before & 0x3FFu), i1 = (int)(mt_new & 0x3FFu);
+            draw_kind = (__ballot(dr_spec && i1 < i0) ? 1u : 0u) | (__ballot(dr_spec && i1 >= i0 && i1 - i0 > 8) ? 2u : 0u);
+        }
+        // commit: lanes whose lock consumed the preview
+        bool dr = draw;
+        if constexpr (TWO) {
+            dr = locknow;
+            if (p.autoreset != ST_AUTORESET_SAME_STEP) {
+                lds_flag_wait(&sm.f1, (uint32_t)t + 1u);
+                const uint32_t w = lane < 32 ? sm.drawm[0] : sm.drawm[1];
+                dr = (w >> (lane & 31)) & 1u;
             }
         }
+        [[maybe_unused]] uint32_t sdd = 0;
+        if (dr) {
+            // (a lane that locks but does not draw keeps its old MT word: the
+            // next-generation words mt_work stored are recomputed identically)
+            ss(ST_STAT_MT_INDEX) = mt_new;
+            atomicAdd(&ss(ST_STAT_COUNT0 + sid), 1u);  // shape_counts[name] += 1, :199 (ds_add, no return)
+            sdd = (1u << ST_STAT_MT_INDEX) | (1u << (ST_STAT_COUNT0 + sid));
+        }
+        if constexpr (KSTEPS == 1) {
+            if constexpr (TWO) sm.SDD[lane] = sdd;
+            else sm.SD[lane] = sdd;  // the logic part ORs its rows in below
+        } else if constexpr (TWO) {
+            sm.mtw[t & 1][lane] = dr ? mt_new : mt0;  // the logic wave's next step reads it after B1
+        }
     }
-    ST_STAMP(5);
 
-    if constexpr (KSTEPS != 1) {
-        // ---- state for the next step: board = obs minus the overlay ----
-        // Erasing the overlaid piece yields the post-step board for every
-        // lane: non-locking lanes and spawns (overlay cells were empty), and a
-        // death without auto-reset (R8: _set_piece(False), tetris_env.py:303).
+    if constexpr (DO_L) {
+        if constexpr (TWO) {
+            // a spawn without a preview takes the draw wave's first draw (rare)
+            const bool need1 = draw && !pv_ok(mt0);
+            if (__ballot(need1)) {
+                lds_flag_wait(&sm.f2, (uint32_t)t + 1u);
+                if (need1) sid = (int)sm.pick1[lane];
+            }
+        }
+        uint32_t pw_out = pack_piece(id, rot, ax, ay, lock);
+        if (draw) pw_out = pack_piece(sid, 0, W / 2, 0, lock);
+        if (spawn) {
+            odesc = tab(sid * 4);
+            oax = W / 2;
+            oay = 0;
+        }
+
+        // ---- counters back to the staged rows (tetris_env.py:253, :264-299) ----
+        if (reset_now) {  // the finished episode's counters (ST_AUTORESET_SAME_STEP)
+            int32_t *st = p.stats + e;
+            st[ST_STAT_EP_TIME * sd] = time;
+            st[ST_STAT_EP_SCORE * sd] = score;
+            st[ST_STAT_EP_LINES * sd] = lines;
+            st[ST_STAT_EP_HOLES * sd] = holes;
+            time = score = lines = holes = height = 0;
+        }
+        // st_step stores only the counter rows that changed (sdirty, per env)
+        [[maybe_unused]] uint32_t sdirty = (1u << ST_STAT_TIME) | (1u << kPieceRow);
+        ss(ST_STAT_TIME) = (uint32_t)time;
+        ss(kPieceRow) = pw_out;
+        if (locknow) {
+            auto put = [&](int r, int32_t v) {
+                if constexpr (KSTEPS == 1) sdirty |= (uint32_t)(ss(r) != (uint32_t)v) << r;
+                ss(r) = (uint32_t)v;
+            };
+            put(ST_STAT_SCORE, score);
+            put(ST_STAT_LINES, lines);
+            put(ST_STAT_HOLES, holes);
+            put(ST_STAT_PIECE_HEIGHT, height);
+            put(ST_STAT_DEATHS, deaths);
+        }
+        if constexpr (KSTEPS == 1) {
+            if constexpr (TWO) sm.SD[lane] = sdirty;
+            else sm.SD[lane] |= sdirty;
+        }
+
+        // ---- observation (tetris_env.py:301-302): board + current piece ----
+        if (KSTEPS != 1 || spawn) paint<S32>(L, lane, odesc.x, odesc.y, oax, oay, hmask);
         wave_sync();
-        erase<S32>(L, lane, odesc.x, odesc.y, oax, oay, hmask);
-        if (reset_now)
-            for (int x = 0; x < W; ++x) lcol(L, x, lane) = floorb;
+        const bool wide_obs = (p.n & 3) == 0 && e0 + kWave <= p.n &&
+                              (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0;
+        if (obs_t && !(kAblate & 8u)) {
+            if (wide_obs) {
+                const uint32_t noff = (uint32_t)lrow * (uint32_t)p.n + (uint32_t)lcc;
+#pragma unroll
+                for (int q = 0; q < NBQ; ++q) {  // interleaved read/store (measured: reads-first
+                                                 // costs the packed rollout ~7%)
+                    if ((WT || 4 * q < W) && 4 * q + lrow < W) {
+                        uint4 v = *reinterpret_cast<const uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]);
+                        v.x &= hmask;
+                        v.y &= hmask;
+                        v.z &= hmask;
+                        v.w &= hmask;
+                        buf_store16<kNT>(buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u),
+                                         ((uint32_t)e0 + (uint32_t)(4 * q) * (uint32_t)p.n + noff) * 4u, v);
+                    }
+                }
+            } else if (real) {  // ragged / unaligned: one dword per row, 32-bit offsets (SGPRs)
+                const auto ro = buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u);
+#pragma unroll 1
+                for (int x = 0; x < W; ++x)
+                    __builtin_amdgcn_raw_buffer_store_b32(lcol(L, x, lane) & hmask, ro,
+                                                          ((uint32_t)x * (uint32_t)p.n + (uint32_t)e) * 4u, 0, kNT);
+            }
+        }
+        if (F32) {
+            // float32 obs [n][W][H] of the wave's envs is one contiguous block,
+            // written as lane-consecutive float4 chunks.
+            const int64_t nreal64 = p.n - e0 < kWave ? p.n - e0 : kWave;
+            const int nreal = (int)nreal64;
+            float *out = p.obs_f32 + ((int64_t)t * p.n + e0) * (W * H);
+            if constexpr (WT != 0 && HT % 4 == 0) {
+                // chunk c = (env, column x, nibble q): 4 floats = bits 4q..4q+3 of
+                // the column word; the float4 comes from the 16-entry table.
+                constexpr int CPC = HT / 4, CPE = WT * CPC;
+                uint32_t *O = sm.O;
+#pragma unroll
+                for (int x = 0; x < WT; ++x) O[lane * (WT + 1) + x] = lcol(L, x, lane) & hmask;
+                wave_sync();
+                float4 *out4 = reinterpret_cast<float4 *>(out);
+                const float4 *F4 = reinterpret_cast<const float4 *>(sm.F4);
+                const int total = nreal * CPE;
+                for (int c = lane; c < total; c += kWave) {
+                    const int ee = c / CPE;
+                    const int cr = c - ee * CPE;
+                    const int x = cr / CPC;
+                    const int q = cr - x * CPC;
+                    const float4 f = F4[(O[ee * (WT + 1) + x] >> (4 * q)) & 15u];
+                    if constexpr (KSTEPS != 1) {
+                        // rollouts: non-temporal (A/B: -13% f32 rollout; the MT and
+                        // state lines stay in L2 instead of the streamed obs; +7% on
+                        // the single-step launch before its other stores were
+                        // made nt, +-0 after, so it keeps plain stores)
+                        typedef float f32x4 __attribute__((ext_vector_type(4)));
+                        const f32x4 fv = {f.x, f.y, f.z, f.w};
+                        __builtin_nontemporal_store(fv, reinterpret_cast<f32x4 *>(&out4[c]));
+                    } else {
+                        out4[c] = f;
+                    }
+                }
+            } else {
+                const int per_env = W * H;
+                const int total = nreal * per_env;
+                auto word = [&](int ee, int x) { return L[(x + kPad) * kWave + ee] & hmask; };
+                for (int f = lane; f < total; f += kWave) {
+                    const int ee = f / per_env;
+                    const int rem = f - ee * per_env;
+                    const int x = rem / H;
+                    const int y = rem - x * H;
+                    out[f] = (float)((word(ee, x) >> y) & 1u);
+                }
+            }
+        }
+        ST_STAMP(5);
+
+        if constexpr (KSTEPS != 1) {
+            // ---- state for the next step: board = obs minus the overlay ----
+            // Erasing the overlaid piece yields the post-step board for every
+            // lane: non-locking lanes and spawns (overlay cells were empty), and a
+            // death without auto-reset (R8: _set_piece(False), tetris_env.py:303).
+            wave_sync();
+            erase<S32>(L, lane, odesc.x, odesc.y, oax, oay, hmask);
+            if (reset_now)
+                for (int x = 0; x < W; ++x) lcol(L, x, lane) = floorb;
+        }
     }
     }  // for t
     wave_sync();
-    if constexpr (KSTEPS != 1) {
+    if constexpr (KSTEPS != 1 && DO_L) {
         // 32-bit buffer offsets: 64-bit row offsets shared with the prologue
         // would stay live (in SGPRs) across the step loop
         const auto rb = buf_rsrc(p.board, (uint32_t)((W + 3) & ~3) * (uint32_t)sd * 4u);
@@ -1028,21 +1256,29 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
             }
         }
     }
-    uint32_t sdl = ~0u;  // rows to store: all (rollout) or those one of the lane's 4 envs changed
+    // counter rows: all (rollout) or those one of the lane's 4 envs changed;
+    // two waves: each stores the rows it owns (logic: 0-5 and the piece row,
+    // draw: the shape counts and the MT word)
+    uint32_t sdl = ~0u;
     if constexpr (KSTEPS == 1) {
-        const uint4 sd4 = *reinterpret_cast<const uint4 *>(&SD[lcc]);
+        const uint32_t *sdm = ROLE == kRoleD ? sm.SDD : sm.SD;
+        const uint4 sd4 = *reinterpret_cast<const uint4 *>(&sdm[lcc]);
         sdl = (sd4.x | sd4.y | sd4.z | sd4.w) >> lrow;
     }
+    constexpr uint32_t kRowsD = ((1u << 7) - 1u) << ST_STAT_COUNT0 | 1u << ST_STAT_MT_INDEX;
+    constexpr uint32_t kOwn = ROLE == kRoleOne ? (1u << kHotRows) - 1u
+                              : ROLE == kRoleD ? kRowsD : ((1u << kHotRows) - 1u) & ~kRowsD;
     const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
     const uint32_t soff = (uint32_t)e0 * 4u + loff * 4u;
 #pragma unroll
     for (int q = 0; q < kHotQ; ++q) {
         // row 15 (ep_time) is never staged: it is stored per lane on a reset
-        const bool st = 4 * q + lrow < kHotRows && ((sdl >> (4 * q)) & 1u);
+        if (((kOwn >> (4 * q)) & 0xFu) == 0u) continue;
+        const bool st = ((kOwn >> (4 * q + lrow)) & 1u) && ((sdl >> (4 * q)) & 1u);
         buf_store16<kNT>(rs, st ? soff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff,
-                    *reinterpret_cast<const uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]));
+                         *reinterpret_cast<const uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]));
     }
-    if constexpr (STAMP && KSTEPS == 1) {
+    if constexpr (STAMP && KSTEPS == 1 && DO_L) {
         ST_STAMP(6);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         ST_STAMP(7);
@@ -1058,14 +1294,20 @@ __device__ __forceinline__ void run_steps(const KParams &p) {
     }
 }
 
+// st_step: two waves per 64 envs (kRoleL, kRoleD), see run_steps.
 template <int WT, int HT, bool F32, bool STAMP = false, bool SC0 = false>
-__global__ __launch_bounds__(kWave) void k_step(KParams p) {
-    run_steps<WT, HT, F32, STAMP, 1, SC0>(p);
+__global__ __launch_bounds__(2 * kWave) void k_step(KParams p) {
+    __shared__ StepLds<F32, 1> sm;
+    if (threadIdx.x < kWave) run_steps<WT, HT, F32, STAMP, 1, SC0, kRoleL>(p, sm);
+    else run_steps<WT, HT, F32, STAMP, 1, SC0, kRoleD>(p, sm);
 }
 
+// st_rollout: the same two waves, handing off once per step.
 template <int WT, int HT, bool F32, bool SC0 = false>
-__global__ __launch_bounds__(kWave) void k_rollout(KParams p) {
-    run_steps<WT, HT, F32, false, 0, SC0>(p);
+__global__ __launch_bounds__(2 * kWave) void k_rollout(KParams p) {
+    __shared__ StepLds<F32, 0> sm;
+    if (threadIdx.x < kWave) run_steps<WT, HT, F32, false, 0, SC0, kRoleL>(p, sm);
+    else run_steps<WT, HT, F32, false, 0, SC0, kRoleD>(p, sm);
 }
 
 // no scoring flags (SC0 specializations of the 10x20 kernels)
@@ -1088,20 +1330,31 @@ __global__ __launch_bounds__(kWave) void k_reset(KParams p) {
 #pragma unroll
     for (int i = 0; i < 7; ++i) cnt[i] = st[(ST_STAT_COUNT0 + i) * sd];
     uint32_t mtst = (uint32_t)st[ST_STAT_MT_INDEX * sd];
+    const uint32_t mt0 = mtst;
     const uint32_t pw = p.piece[e];
     const MtPre nopre{};
-    const int pick = draw_shape<8>(m, cnt, mtst, p.mt + e0 * kMtPitch, S, lane, nopre, false);
+    // the new piece: the preview, or (none valid) a draw; then the next preview
+    int sid = pv_id(mt0);
+    const bool need1 = m && !pv_ok(mt0);
+    if (__ballot(need1)) {
+        const int pk = draw_shape<8, false>(need1, cnt, mtst, p.mt + e0 * kMtPitch, S, lane, nopre, false);
+        if (need1) sid = pk;
+    }
+#pragma unroll
+    for (int i = 0; i < 7; ++i) cnt[i] += (m && i == sid);  // _new_piece :199
+    const uint32_t m1 = mtst;
+    const int npv = draw_shape<8, false>(m, cnt, mtst, p.mt + e0 * kMtPitch, S, lane, nopre, false);
     if (m) {
         st[ST_STAT_TIME * sd] = 0;
         st[ST_STAT_SCORE * sd] = 0;
         st[ST_STAT_HOLES * sd] = 0;
         st[ST_STAT_LINES * sd] = 0;
         st[ST_STAT_PIECE_HEIGHT * sd] = 0;
-        st[ST_STAT_MT_INDEX * sd] = (int32_t)mtst;
+        st[ST_STAT_MT_INDEX * sd] = (int32_t)pv_pack(mtst, npv, mt_consumed(m1, mtst));
 #pragma unroll
         for (int i = 0; i < 7; ++i) st[(ST_STAT_COUNT0 + i) * sd] = cnt[i];
         for (int x = 0; x < p.W; ++x) p.board[x * sd + e] = 0u;
-        p.piece[e] = pack_piece(pick, 0, p.W / 2, 0, (int)(pw >> 17));
+        p.piece[e] = pack_piece(sid, 0, p.W / 2, 0, (int)(pw >> 17));
     }
 }
 
@@ -1165,16 +1418,32 @@ __global__ void k_seed(KParams p) {
 
 // ---------------------------------------------------------------- MT sync
 // st_mt_sync: every env back to CPython's form (see "Double-buffered twist"):
-// where the current generation is in B, B is copied to A; the index loses the
-// engine bits (the next generation's progress restarts at 0).  One wave per
-// 64 envs; it copies its lanes' B buffers one env at a time, cooperatively.
+// the preview's words are given back (the reference has not drawn it: its
+// state is c words earlier, in the previous generation if the preview's draw
+// crossed index 624 -- that buffer is intact, no next-generation block has
+// been built since the switch), the generation holding that position is
+// copied to A if it is B, and the index loses the engine bits (the next
+// generation's progress restarts at 0, the preview is dropped: the next spawn
+// draws its piece, then a new preview).  One wave per 64 envs; it copies its
+// lanes' B buffers one env at a time, cooperatively.
 __global__ __launch_bounds__(kWave) void k_mt_sync(KParams p) {
     const int lane = threadIdx.x;
     const int64_t e0 = (int64_t)blockIdx.x * kWave;
     const int64_t e = e0 + lane;
     int32_t *row = p.stats + (int64_t)ST_STAT_MT_INDEX * p.stride;
     const uint32_t r = (uint32_t)row[e];
-    uint64_t inb = __ballot((r >> 20) & 1u);
+    int idx = (int)(r & 0x3FFu);
+    uint32_t cur = (r >> 20) & 1u;
+    if (pv_ok(r)) {
+        const int c = (int)(r >> 25);
+        if (idx >= c) {
+            idx -= c;
+        } else {
+            idx = kMtN - (c - idx);
+            cur ^= 1u;
+        }
+    }
+    uint64_t inb = __ballot(cur);
     while (inb) {
         const int l = __builtin_ctzll(inb);
         inb &= inb - 1;
@@ -1191,7 +1460,7 @@ __global__ __launch_bounds__(kWave) void k_mt_sync(KParams p) {
             if (i < kMtN) g[i] = t[q];
         }
     }
-    if ((r >> 10) != 0u) row[e] = (int32_t)(r & 0x3FFu);
+    if (r != (uint32_t)idx) row[e] = idx;
 }
 
 // ---------------------------------------------------------------- render
@@ -1377,7 +1646,7 @@ hipError_t launch_reset(const KParams &p, hipStream_t s) {
 }
 
 hipError_t launch_step(const KParams &p, hipStream_t s) {
-    const dim3 grid((unsigned)(p.stride / kWave)), block(kWave);
+    const dim3 grid((unsigned)(p.stride / kWave)), block(2 * kWave);  // logic + draw wave
     const bool f32 = p.obs_f32 != nullptr;
     const bool sc0 = !(p.flags & kScoringFlags);
     if (p.stamps && p.W == 10 && p.H == 20) {
@@ -1407,7 +1676,7 @@ hipError_t launch_render(const KParams &p, hipStream_t s) {
 }
 
 hipError_t launch_rollout(const KParams &p, hipStream_t s) {
-    const dim3 grid((unsigned)(p.stride / kWave)), block(kWave);
+    const dim3 grid((unsigned)(p.stride / kWave)), block(2 * kWave);  // logic + draw wave
     const bool f32 = p.obs_f32 != nullptr;
     const bool sc0 = !(p.flags & kScoringFlags);
     if (p.W == 10 && p.H == 20) {

@@ -2,7 +2,7 @@
 # GPU parity tests + a short bench (all variants) + SQ instruction counters.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"; mkdir -p gpurun_out; TAG=${TAG:-q}
-timeout -k 10 500 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_$TAG.log 2>&1; rc=$?
+timeout -k 10 500 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1; rc=$?
 tail -2 gpurun_out/pytest_$TAG.log; grep -m3 "^E " gpurun_out/pytest_$TAG.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python bench.py --steps 500 --warmup 50 --no-cpu-baseline \
