@@ -17,9 +17,10 @@ constexpr int kMtN = 624;
 constexpr int64_t kMtPitch = 2 * kMtN + 16;
 // after the last env: a draw window reads up to 16 words past index 623 of B
 constexpr int64_t kMtPadBack = 64;
-// diagnostic stamps per wave: 10 s_memtime phase stamps, s_memrealtime at
-// start and end, HW_ID, XCC_ID (16 words)
-constexpr int kStampWords = 16;
+// diagnostic stamps per workgroup: logic wave 10 s_memtime phase stamps,
+// s_memrealtime at start and end, HW_ID, XCC_ID, draw kind (words 0-15); draw
+// wave 12 stamps + s_memrealtime at start and end (words 16-31)
+constexpr int kStampWords = 32;
 constexpr int kPieceRow = ST_STAT_PIECE;     // rows 0..14 (counters + piece) move every step
 constexpr int kHotRows = ST_STAT_PIECE + 1;
 constexpr int kHotQ = (kHotRows * 16 + kWave - 1) / kWave;  // 16-B slots per lane
@@ -42,7 +43,8 @@ struct KParams {
     uint32_t *board;    // [W][stride]
     uint32_t *piece;    // [stride]
     int32_t *stats;     // [ST_NSTAT][stride]
-    uint32_t *mt;       // [stride][624]
+    uint32_t *mt;       // [stride][kMtPitch]
+    uint32_t *mtc;      // [stride][4] draw-window cache (see st_kernels.hip, MT word)
     // io
     const uint8_t *actions;  // [n]
     const uint8_t *mask;     // [n] (reset) or null

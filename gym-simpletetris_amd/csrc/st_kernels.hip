@@ -127,6 +127,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uin
 // `nt` stores stream out during the kernel instead (A/B, st_step packed:
 // 6.31 -> 5.89 us with obs, board, counter and MT stores all `nt`).
 constexpr int kNT = 2;
+// A/B knobs: issue priority of the st_step draw wave after B1 (0 = default;
+// rollouts use 2), and which st_step wave builds the next-generation block
+// (1: the logic wave)
+#ifndef ST_DPRIO
+#define ST_DPRIO 0
+#endif
+#ifndef ST_LWORK
+#define ST_LWORK 0
+#endif
 template <int AUX = 0>
 __device__ __forceinline__ void buf_store16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
     const i32x4 d = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
@@ -270,13 +279,16 @@ __device__ __forceinline__ uint32_t mt_pack(int idx, int pg, int cur) {
 }
 // The preview (the piece the env's NEXT spawn takes, drawn one spawn ahead so
 // that no step waits on a draw; see run_steps) in the upper bits of the same
-// word: pv << 21 | ok << 24 | c << 25, c = the MT words its draw consumed,
-// so the reference's state -- the one before the preview was drawn -- is c
-// words back (k_mt_sync).  ok = 0 (a host-written or synced state): the next
-// spawn draws its piece first, then the preview.
+// word: pv << 21 | ok << 24 | c << 25 | cv << 31, c = the MT words its draw
+// consumed (6 bits; a draw of > 62 words has p < 2^-62), so the reference's
+// state -- the one before the preview was drawn -- is c words back
+// (k_mt_sync).  ok = 0 (a host-written or synced state): the next spawn draws
+// its piece first, then the preview.  cv: the env's 4-word draw-window cache
+// (KParams::mtc) holds words idx..idx+3 of the current generation.
 constexpr uint32_t kMtLow = (1u << 21) - 1u;  // idx | pg | cur
 constexpr uint32_t kPvOk = 1u << 24;
-constexpr uint32_t kPvCMax = 127u;
+constexpr uint32_t kPvCMax = 63u;
+constexpr uint32_t kCv = 1u << 31;
 __device__ __forceinline__ uint32_t mt_keep(uint32_t hi, uint32_t low) { return (hi & ~kMtLow) | low; }
 __device__ __forceinline__ int pv_id(uint32_t r) { return (int)((r >> 21) & 7u); }
 __device__ __forceinline__ bool pv_ok(uint32_t r) { return (r & kPvOk) != 0u; }
@@ -287,9 +299,10 @@ __device__ __forceinline__ uint32_t mt_consumed(uint32_t before, uint32_t after)
     const int c = ((before ^ after) >> 20) & 1u ? kMtN - i0 + i1 : i1 - i0;
     return (uint32_t)c < kPvCMax ? (uint32_t)c : kPvCMax;
 }
-__device__ __forceinline__ uint32_t pv_pack(uint32_t mt_after, int pv, uint32_t c) {
-    return (mt_after & kMtLow) | ((uint32_t)pv << 21) | kPvOk | (c << 25);
+__device__ __forceinline__ uint32_t pv_pack(uint32_t mt_after, int pv, uint32_t c, bool cv = false) {
+    return (mt_after & kMtLow) | ((uint32_t)pv << 21) | kPvOk | (c << 25) | (cv ? kCv : 0u);
 }
+__device__ __forceinline__ bool cache_ok(uint32_t r) { return (r & (kPvOk | kCv)) == (kPvOk | kCv); }
 
 // The wave's 64 MT states as one buffer resource.  Loads and stores of lanes
 // (or operands) not wanted get an out-of-range offset (loads read 0), so each
@@ -318,34 +331,40 @@ struct MtPre {
 };
 // WIN = 16 for st_step; 8 in rollouts, where the second half measured slower
 // (register pressure in the k-step loop).
-template <int WIN>
-__device__ __forceinline__ void mt_pre_load(const MtRes &rs, uint32_t mtst, bool want, MtPre &q) {
+// WIN: window words (0: none); OPS: the block operands.  (st_step: the draw
+// wave loads the window, the logic wave the operands.)
+template <int WIN, bool OPS = true>
+__device__ __forceinline__ void mt_pre_load(const MtRes &rs, uint32_t mtst, bool want, MtPre &q, int woff = 0) {
     int idx, pg, cur;
     mt_unpack(mtst, idx, pg, cur);
     const uint32_t cb = cur ? kMtB : 0u, nb = cur ? 0u : kMtB;
     const bool work = want && pg < kMtN;
-    u32x4 wv[WIN / 4];
+    u32x4 wv[WIN > 0 ? WIN / 4 : 1];
 #pragma unroll
-    for (int i = 0; i < WIN / 4; ++i) wv[i] = mt_ld16(rs, want, cb + idx + 4 * i);
-    const u32x4 a = mt_ld16(rs, work, cb + pg);
-    const u32x4 x = mt_ld16(rs, work, pg <= 224 ? cb + pg + 397 : nb + pg - 227);
-    q.a[4] = __builtin_amdgcn_raw_buffer_load_b32(rs.r, work ? rs.lane_off + 4u * (cb + pg + 4) : kOff, 0, 0);
+    for (int i = 0; i < WIN / 4; ++i) wv[i] = mt_ld16(rs, want, cb + idx + woff + 4 * i);
+    if constexpr (OPS) {
+        const u32x4 a = mt_ld16(rs, work, cb + pg);
+        const u32x4 x = mt_ld16(rs, work, pg <= 224 ? cb + pg + 397 : nb + pg - 227);
+        q.a[4] = __builtin_amdgcn_raw_buffer_load_b32(rs.r, work ? rs.lane_off + 4u * (cb + pg + 4) : kOff, 0, 0);
+        q.a[0] = a.x, q.a[1] = a.y, q.a[2] = a.z, q.a[3] = a.w;
+        q.x[0] = x.x, q.x[1] = x.y, q.x[2] = x.z, q.x[3] = x.w;
+    }
 #pragma unroll
     for (int i = 0; i < WIN / 4; ++i)
         q.w[4 * i] = wv[i].x, q.w[4 * i + 1] = wv[i].y, q.w[4 * i + 2] = wv[i].z, q.w[4 * i + 3] = wv[i].w;
-    q.a[0] = a.x, q.a[1] = a.y, q.a[2] = a.z, q.a[3] = a.w;
-    q.x[0] = x.x, q.x[1] = x.y, q.x[2] = x.z, q.x[3] = x.w;
 }
 // Take all prefetched words at once (one vmcnt wait on a single path): words
 // never read would stay "pending" for the compiler, and every later reuse of
 // their registers would wait vmcnt(0), draining the step's early stores.
 template <int WIN>
-__device__ __forceinline__ void mt_pre_consume(const MtPre &q) {
+__device__ __forceinline__ void mt_win_consume(const MtPre &q) {
     asm volatile("" ::"v"(q.w[0]), "v"(q.w[1]), "v"(q.w[2]), "v"(q.w[3]), "v"(q.w[4]), "v"(q.w[5]),
                  "v"(q.w[6]), "v"(q.w[7]));
     if constexpr (WIN > 8)
         asm volatile("" ::"v"(q.w[8]), "v"(q.w[9]), "v"(q.w[10]), "v"(q.w[11]), "v"(q.w[12]),
                      "v"(q.w[13]), "v"(q.w[14]), "v"(q.w[15]));
+}
+__device__ __forceinline__ void mt_ops_consume(const MtPre &q) {
     asm volatile("" ::"v"(q.a[0]), "v"(q.a[1]), "v"(q.a[2]), "v"(q.a[3]), "v"(q.a[4]), "v"(q.x[0]),
                  "v"(q.x[1]), "v"(q.x[2]), "v"(q.x[3]));
 }
@@ -432,10 +451,17 @@ __device__ __attribute__((noinline)) void mt_finish(uint32_t *g, uint32_t *S, in
 // continue in the loop, switching generations at index 624.
 // COUNT: also count the drawn shape in cnt (a spawn's _new_piece :199; not
 // for a preview, which is counted when it spawns).
-template <int WIN, bool COUNT = true>
+// CACHED: lanes with `cv` first try the 4 cached words c4 (positions
+// idx..idx+3, no load to wait for); the window then sits at idx + woff
+// (woff = 4 for those lanes) and is waited for only if some lane needs it.
+// *fastpos: the position after the draw (before a generation switch) when the
+// prefetched words settled it, else -1.
+template <int WIN, bool COUNT = true, bool CACHED = false>
 __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t &mtst,
                                           uint32_t *mt_wave, uint32_t *S, int lane,
-                                          const MtPre &pre, bool have_pre) {
+                                          const MtPre &pre, bool have_pre,
+                                          const uint32_t *c4 = nullptr, bool cv = false, int woff = 0,
+                                          int *fastpos = nullptr) {
     int32_t maxc = cnt[0], sumc = cnt[0];
 #pragma unroll
     for (int i = 1; i < 7; ++i) {
@@ -448,39 +474,51 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
     mt_unpack(mtst, idx, pg, cur);
     bool pending = need;
     uint32_t r = 0;
-    mt_pre_consume<WIN>(pre);
+    if constexpr (!CACHED) mt_win_consume<WIN>(pre);
+    int fpos = -1;
     if (have_pre && pending) {
         // The prefetched words sit at positions idx.. of the current
         // generation and, past 623, of the next one (cur[624..639] is
         // next[0..15], see the layout) -- usable there once it is complete.
         const int lim = pg == kMtN ? kMtN + WIN : kMtN;
         int pos = idx;  // words consumed, counted from the current generation's start
-        auto pass = [&](int j0) {
-            int first = 8;
+        // NW words w[0..NW) at positions p0.. (lanes continuing at p0 only)
+        auto pass = [&](const uint32_t *w, int p0, auto nwc) {
+            constexpr int NW = decltype(nwc)::value;
+            int first = NW;
             uint32_t rr = 0;
 #pragma unroll
-            for (int j = 7; j >= 0; --j) {
-                const uint32_t y = mt_temper(pre.w[j0 + j]) >> (32 - kb);
-                const bool acc = y < n && idx + j0 + j < lim;
+            for (int j = NW - 1; j >= 0; --j) {
+                const uint32_t y = mt_temper(w[j]) >> (32 - kb);
+                const bool acc = y < n && p0 + j < lim;
                 first = acc ? j : first;
                 rr = acc ? y : rr;
             }
-            if (first < 8) {
+            if (first < NW) {
                 pending = false;
                 r = rr;
-                pos = idx + j0 + first + 1;
+                pos = p0 + first + 1;
             } else {
-                pos = idx + j0 + 8 < lim ? idx + j0 + 8 : lim;
+                pos = p0 + NW < lim ? p0 + NW : lim;
             }
         };
-        pass(0);
+        using I4 = std::integral_constant<int, 4>;
+        using I8 = std::integral_constant<int, 8>;
+        if constexpr (CACHED) {
+            if (cv) pass(c4, idx, I4{});
+        }
+        const int b = idx + woff;
+        if (!CACHED || __ballot(pending && pos == b)) {
+            if (pending && pos == b) pass(pre.w, b, I8{});
+        }
         // 8 rejections in a row (p <= 2^-8 per draw, a few lanes per step):
         // the next 8 words are already here, no dependent load
         if constexpr (WIN > 8) {
-            if (__ballot(pending && pos == idx + 8)) {
-                if (pending && pos == idx + 8) pass(8);
+            if (__ballot(pending && pos == b + 8)) {
+                if (pending && pos == b + 8) pass(pre.w + 8, b + 8, I8{});
             }
         }
+        if (!pending) fpos = pos;
         if (pos > kMtN) {  // the draw ran into the (complete) next generation
             cur ^= 1;
             pos -= kMtN;
@@ -507,6 +545,11 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
             }
             const uint32_t cb = cur ? kMtB : 0u;
             const u32x4 w0 = mt_ld16(rs, pending, cb + idx), w1 = mt_ld16(rs, pending, cb + idx + 4);
+            // both consumed here: the loop below may break before reading w1,
+            // and a load still pending at the exit makes every later write of
+            // its registers (reused by the caller) wait vmcnt(0)
+            asm volatile("" ::"v"(w0.x), "v"(w0.y), "v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w1.z),
+                         "v"(w1.w));
             const uint32_t word[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -523,6 +566,7 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
         } while (__ballot(pending));
     }
     if (need) mtst = mt_keep(mtst, mt_pack(idx, pg, cur));
+    if (fastpos) *fastpos = fpos;
     if (!need) return 0;
     int32_t rr = (int32_t)r + 1;
     int pick = 6;
@@ -586,6 +630,9 @@ struct StepLds {
     // before the other has read step t's)
     uint32_t lockm[2][2], drawm[2];
     uint32_t pick1[kWave];
+    // st_step draw wave: per lane [cache 4 | window 16] words, to pick the
+    // next cache (4 words at the new position) by a dynamic offset
+    uint32_t cw[KSTEPS == 1 ? kWave * 20 : 4] __attribute__((aligned(16)));
     uint32_t mtw[2][KSTEPS == 1 ? 1 : kWave];  // rollouts: the draw wave's MT word after step t
     uint32_t f1, f2;  // = t + 1 once step t's draw mask / first picks are written
 };
@@ -618,16 +665,20 @@ __device__ __forceinline__ void wg_barrier() {
 // outstanding global stores are not drained).
 // (LDS address space explicitly: through a generic pointer the accesses
 // become flat_* instructions, which count in vmcnt and wait for it.)
-typedef __attribute__((address_space(3))) volatile uint32_t lds_vu32;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+// (Relaxed atomics + compiler-only fences: a volatile access or an asm memory
+// clobber here makes the compiler wait for every outstanding load first --
+// vmcnt(0) -- which cost the draw wave its whole MT-window latency.)
 __device__ __forceinline__ void lds_flag_set(uint32_t *f, uint32_t v) {
-    asm volatile("" ::: "memory");
-    *(lds_vu32 *)f = v;
-    asm volatile("" ::: "memory");
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __hip_atomic_store((lds_u32 *)f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 __device__ __forceinline__ void lds_flag_wait(uint32_t *f, uint32_t v) {
-    asm volatile("" ::: "memory");
-    while (*(lds_vu32 *)f != v) __builtin_amdgcn_s_sleep(1);
-    asm volatile("" ::: "memory");
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    while (__hip_atomic_load((lds_u32 *)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != v)
+        __builtin_amdgcn_s_sleep(1);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
 // KSTEPS == 1: TetrisEngine.step once (st_step), ROLE = kRoleL / kRoleD (the
@@ -644,7 +695,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
     constexpr bool DO_L = ROLE != kRoleD;  // action, lock path, outputs
     constexpr bool DO_D = ROLE != kRoleL;  // MT words, next-generation block, draws
     constexpr bool TWO = ROLE != kRoleOne;
-    [[maybe_unused]] uint64_t tstamp[10] = {};
+    [[maybe_unused]] uint64_t tstamp[12] = {};
     [[maybe_unused]] uint64_t draw_kind = 0;  // stamp build: 1 = a lane twisted, 2 = a draw ran past 8 words
     constexpr bool S32 = HT != 0 && HT <= 25;  // see pc_bits
     const uint32_t kFlags = SC0 ? (p.flags & (ST_REWARD_STEP | ST_STEP_RESET)) : p.flags;
@@ -707,10 +758,17 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         if (mine_q(q))
             sv[q] = *reinterpret_cast<const uint4 *>(ssrc + (size_t)(4 * q) * sd +
                                                      (4 * q + 4 <= kHotRows ? loff : clamp_off(q, kHotRows)));
+    [[maybe_unused]] uint4 c4v = make_uint4(0u, 0u, 0u, 0u);
     const int K = KSTEPS ? KSTEPS : p.k;
+    // two-wave st_step: the logic wave also builds the next-generation block
+    // (the draw wave's chain is the longer one).  (Measured and dropped: the
+    // draw wave running the action phase itself instead of waiting at B1 --
+    // the two concurrent action phases slowed the logic wave's by ~50%.)
+    constexpr bool STEP2 = TWO && KSTEPS == 1;
+    constexpr bool ACT = DO_L;
     // unconditional (clamped) so it is issued with the others; masked at use
     uint32_t act_next = 0;
-    if constexpr (DO_L) act_next = p.actions[real ? e : p.n - 1];
+    if constexpr (ACT) act_next = p.actions[real ? e : p.n - 1];
     // The piece table, lane i = entry i, from immediates by compare/select
     // (VALU under the load latency; no memory access: a __constant__ load
     // gets sunk by the compiler past the state loads' completion -- one more
@@ -774,6 +832,9 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         if (ROLE == kRoleL && lane == 0) sm.f1 = 0u;
         if (ROLE == kRoleD && lane == 0) sm.f2 = 0u;
         wg_barrier();  // B0: the staged state is complete
+        // the draw wave's cache words: loaded now (not in the prologue's
+        // burst), they arrive while it waits for the lock ballot at B1
+        if constexpr (KSTEPS == 1 && ROLE == kRoleD) c4v = *reinterpret_cast<const uint4 *>(p.mtc + 4 * e);
     } else {
         wave_sync();
     }
@@ -783,7 +844,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
     for (int t = 0; t < K; ++t) {
     // ---------------- logic: action, gravity, lock decision ----------------
     uint32_t act = 6u;
-    if constexpr (DO_L) {
+    if constexpr (ACT) {
         act = real ? act_next : 6u;
         if (KSTEPS != 1 && t + 1 < K) act_next = p.actions[(int64_t)(t + 1) * p.n + (real ? e : p.n - 1)];
     }
@@ -805,7 +866,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
     uint2 desc = make_uint2(0u, 0u);
     bool locknow = false;
     int32_t rew = 0;
-    if constexpr (DO_L) {
+    if constexpr (ACT) {
         // ---- action (tetris_env.py:245; value_action_map :152-160) + drop ----
         // Current and candidate descriptors and their columns are read in one
         // LDS round trip each; the collision and drop tests are then pure VALU.
@@ -858,6 +919,10 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
             }
         }
         wg_barrier();  // B1: the draw wave learns which lanes lock
+        if constexpr (DO_D) ST_STAMP(10);
+        // the draw wave's chain is the critical one after B1 (rollouts: -6%)
+        constexpr int kDPrio = KSTEPS == 1 ? ST_DPRIO : 2;
+        if constexpr (DO_D && kDPrio > 0) __builtin_amdgcn_s_setprio(kDPrio);
         if constexpr (DO_D) {
             const uint32_t w = lane < 32 ? sm.lockm[t & 1][0] : sm.lockm[t & 1][1];
             locknow = (w >> (lane & 31)) & 1u;
@@ -877,9 +942,23 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
     constexpr int kWin = KSTEPS == 1 || TWO ? 16 : 8;
     MtPre pre;
     [[maybe_unused]] MtRes mrs;
+    // st_step: lanes whose draw-window cache is valid take their first 4 words
+    // from it (loaded with the state) and load the window 4 words further on
+    constexpr bool LWORK = STEP2 && ST_LWORK;
+    [[maybe_unused]] const bool cv = STEP2 && cache_ok(mt0);
+    [[maybe_unused]] const int woff = cv ? 4 : 0;
     if constexpr (DO_D) {
+        // the cache words to the lane's LDS row before the window loads are
+        // issued: their wait is here, not after the draw's branchy first-draw
+        // path, where it would become a vmcnt(0) on the window
+        if constexpr (STEP2) *reinterpret_cast<uint4 *>(&sm.cw[lane * 20]) = c4v;
         mrs = mt_res(p.mt + e0 * kMtPitch, lane);
-        mt_pre_load<kWin>(mrs, mtst, want_pre, pre);
+        if constexpr (LWORK) mt_pre_load<kWin, false>(mrs, mtst, want_pre, pre, woff);  // window only
+        else mt_pre_load<kWin>(mrs, mtst, want_pre, pre, woff);
+    }
+    if constexpr (LWORK && DO_L) {  // the logic wave builds the next-generation block
+        mrs = mt_res(p.mt + e0 * kMtPitch, lane);
+        mt_pre_load<0>(mrs, mtst, want_pre, pre);
     }
 
     // ---------------- logic: lock path (tetris_env.py:263-299) ----------------
@@ -1029,6 +1108,16 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         }
         wave_sync();  // the board reads above precede the overlay paint
         if (!spawn) paint<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
+        if constexpr (LWORK) {
+            // next[pg..pg+3] (the draw wave counts it done in the MT word it
+            // commits; its own draws treat the block as pending: a finish it
+            // may run rewrites the same values)
+            if (!(kAblate & 2u)) {
+                mt_ops_consume(pre);
+                uint32_t mtw = mt0;
+                mt_work<kNT>(mrs, want_pre, mtw, pre);
+            }
+        }
     }
 
     ST_STAMP(8);  // (stamp 8: between the early stores and the draw)
@@ -1043,14 +1132,19 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
 #pragma unroll
         for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)ss(ST_STAT_COUNT0 + i);  // used by drawing lanes only
         if constexpr (STAMP) {  // diagnostic split of the draw: MT-word wait | compute
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if constexpr (!STEP2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (st_step: the cache pass does not wait)
             ST_STAMP(9);
         }
         [[maybe_unused]] const uint32_t mt_before = mtst;
         uint32_t mt_new = mtst;
+        [[maybe_unused]] bool cvn = false;
+        [[maybe_unused]] uint4 n4 = make_uint4(0u, 0u, 0u, 0u);
         if (!(kAblate & 2u)) {
-            mt_pre_consume<kWin>(pre);
-            mt_work<KSTEPS == 1 ? kNT : 0>(mrs, want_pre, mtst, pre);  // before the draws: a switch resets the progress
+            if constexpr (!STEP2) {
+                mt_win_consume<kWin>(pre);
+                mt_ops_consume(pre);
+                mt_work<KSTEPS == 1 ? kNT : 0>(mrs, want_pre, mtst, pre);  // before the draws: a switch resets the progress
+            }
             const bool need1 = dr_spec && !pv_ok(mt0);
             if (__ballot(need1)) {  // rare: after st_seed / st_mt_sync / a host-written state
                 const int pk = draw_shape<kWin, false>(need1, cnt, mtst, p.mt + e0 * kMtPitch, sm.S, lane, pre, false);
@@ -1063,9 +1157,40 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
 #pragma unroll
             for (int i = 0; i < 7; ++i) cnt[i] += (dr_spec && i == sid);  // _new_piece :199
             const uint32_t m0 = mtst;
-            const int npv = draw_shape<kWin, false>(dr_spec, cnt, mtst, p.mt + e0 * kMtPitch, sm.S, lane, pre,
-                                                     want_pre && pv_ok(mt0));
-            mt_new = pv_pack(mtst, npv, mt_consumed(m0, mtst));
+            int fpos = -1;
+            const uint32_t c4a[4] = {c4v.x, c4v.y, c4v.z, c4v.w};
+            const int npv = draw_shape<kWin, false, STEP2>(dr_spec, cnt, mtst, p.mt + e0 * kMtPitch, sm.S, lane,
+                                                            pre, want_pre && pv_ok(mt0), c4a, cv, woff, &fpos);
+            if constexpr (STEP2) {
+                // the next cache: the 4 words at the new position, picked from
+                // [cache | window] (positions i0.. of the draw's start) through
+                // a per-lane LDS row; valid only if the fast passes settled the
+                // draw and the 4 words lie inside the window and below lim
+                uint32_t *row = &sm.cw[lane * 20];  // row[0..3] = the cache (prologue)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    *reinterpret_cast<uint4 *>(row + woff + 4 * q) =
+                        make_uint4(pre.w[4 * q], pre.w[4 * q + 1], pre.w[4 * q + 2], pre.w[4 * q + 3]);
+                int i0, pg0, c0;
+                mt_unpack(m0, i0, pg0, c0);
+                const int lim0 = pg0 == kMtN ? kMtN + kWin : kMtN;
+                const int off = fpos - i0;
+                cvn = fpos >= 0 && off + 3 <= woff + 15 && fpos + 3 < lim0;
+                const int o = cvn ? off : 0;
+                n4 = make_uint4(row[o], row[o + 1], row[o + 2], row[o + 3]);
+                if constexpr (!LWORK) {  // the block, after the draw (its operands arrived under it)
+                    mt_ops_consume(pre);
+                    uint32_t mtw = mt0;
+                    mt_work<kNT>(mrs, want_pre, mtw, pre);
+                }
+                // this step's block counts unless a draw switched generations
+                // (which restarts the progress at 0)
+                int i1, pg1, c1, ia, pga, ca;
+                mt_unpack(mtst, i1, pg1, c1);
+                mt_unpack(mt0, ia, pga, ca);
+                if (want_pre && c1 == ca && pga < kMtN) mtst = mt_keep(mtst, mt_pack(i1, pga + 4, c1));
+            }
+            mt_new = pv_pack(mtst, npv, mt_consumed(m0, mtst), cvn);
         } else if constexpr (TWO) {
             sm.pick1[lane] = (uint32_t)sid;
             if (lane == 0) lds_flag_set(&sm.f2, (uint32_t)t + 1u);
@@ -1086,6 +1211,10 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
             }
         }
         [[maybe_unused]] uint32_t sdd = 0;
+        if constexpr (STEP2) {  // the next draw-window cache (lanes that drew and have one)
+            const auto rc = buf_rsrc(p.mtc, (uint32_t)sd * 16u);
+            buf_store16<kNT>(rc, dr && cvn ? (uint32_t)e * 16u : kOff, n4);
+        }
         if (dr) {
             // (a lane that locks but does not draw keeps its old MT word: the
             // next-generation words mt_work stored are recomputed identically)
@@ -1099,6 +1228,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         } else if constexpr (TWO) {
             sm.mtw[t & 1][lane] = dr ? mt_new : mt0;  // the logic wave's next step reads it after B1
         }
+        ST_STAMP(11);
     }
 
     if constexpr (DO_L) {
@@ -1110,6 +1240,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
                 if (need1) sid = (int)sm.pick1[lane];
             }
         }
+        ST_STAMP(4);
         uint32_t pw_out = pack_piece(id, rot, ax, ay, lock);
         if (draw) pw_out = pack_piece(sid, 0, W / 2, 0, lock);
         if (spawn) {
@@ -1278,18 +1409,29 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         buf_store16<kNT>(rs, st ? soff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff,
                          *reinterpret_cast<const uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]));
     }
-    if constexpr (STAMP && KSTEPS == 1 && DO_L) {
+    if constexpr (STAMP && KSTEPS == 1) {
+        // words [0, 16) of the workgroup's slot: the logic wave (stamps
+        // 0-9, realtime start/end, HW_ID, XCC_ID, draw kind); [16, 32): the
+        // draw wave (stamps 0-11, realtime start/end)
         ST_STAMP(6);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         ST_STAMP(7);
+        uint64_t *slot = p.stamps + (int64_t)blockIdx.x * kStampWords + (ROLE == kRoleD ? 16 : 0);
         if (lane == 0) {
+            if constexpr (ROLE == kRoleD) {
 #pragma unroll
-            for (int i = 0; i < 10; ++i) p.stamps[blockIdx.x * kStampWords + i] = tstamp[i];
-            p.stamps[blockIdx.x * kStampWords + 10] = rt0;
-            p.stamps[blockIdx.x * kStampWords + 11] = __builtin_amdgcn_s_memrealtime();
-            p.stamps[blockIdx.x * kStampWords + 12] = __builtin_amdgcn_s_getreg(0xF804);  // HW_ID
-            p.stamps[blockIdx.x * kStampWords + 13] = __builtin_amdgcn_s_getreg(0xF814);  // XCC_ID
-            p.stamps[blockIdx.x * kStampWords + 14] = draw_kind;
+                for (int i = 0; i < 12; ++i) slot[i] = tstamp[i];
+                slot[12] = rt0;
+                slot[13] = __builtin_amdgcn_s_memrealtime();
+                slot[14] = draw_kind;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 10; ++i) slot[i] = tstamp[i];
+                slot[10] = rt0;
+                slot[11] = __builtin_amdgcn_s_memrealtime();
+                slot[12] = __builtin_amdgcn_s_getreg(0xF804);  // HW_ID
+                slot[13] = __builtin_amdgcn_s_getreg(0xF814);  // XCC_ID
+            }
         }
     }
 }
@@ -1435,7 +1577,7 @@ __global__ __launch_bounds__(kWave) void k_mt_sync(KParams p) {
     int idx = (int)(r & 0x3FFu);
     uint32_t cur = (r >> 20) & 1u;
     if (pv_ok(r)) {
-        const int c = (int)(r >> 25);
+        const int c = (int)((r >> 25) & kPvCMax);
         if (idx >= c) {
             idx -= c;
         } else {

@@ -17,19 +17,24 @@ n = 65536
 b = G.TetrisBatch(n, autoreset="same_step", seeds=[1000 + e for e in range(n)])
 b.reset()
 nw = b.stride // 64
-W = 16  # kStampWords
+W = 32  # kStampWords: logic wave words 0-15, draw wave 16-31
 buf = np.zeros(nw * W, np.uint64)
 rts = []
-names = ["loads", "action+drop", "lock path", "early stores", "store+MT wait", "draw", "obs (+f32) issue", "state stores issue", "store drain"]
-acc = []
+# logic wave: stamps 0 1 2 3 8 4 5 6 7 (8 sits between 3 and 4)
+names = ["loads+B0", "action+drop", "B1+lock path", "early stores", "spawn-id wait", "obs+counters", "state stores issue", "store drain"]
+# draw wave: stamps 0 1 2 10 9 4 11 6 7
+dnames = ["loads+B0", "until L's action", "B1", "MT words wait", "draws", "commit", "state stores issue", "store drain"]
+acc, dacc = [], []
 
 
 def record():
     b._L.st_debug_stamps(b._ctx, ctypes.c_void_p(buf.ctypes.data), buf.size)
     full = buf.reshape(nw, W).astype(np.int64)
-    st = full[:, [0, 1, 2, 3, 8, 9, 4, 5, 6, 7]]  # stamps 8, 9 sit between 3 and 4
-    acc.append(np.diff(st, axis=1))
-    rts.append(full[:, 10:15].copy())
+    acc.append(np.diff(full[:, [0, 1, 2, 3, 8, 4, 5, 6, 7]], axis=1))
+    dacc.append(np.diff(full[:, [16 + i for i in (0, 1, 2, 10, 9, 4, 11, 6, 7)]], axis=1))
+    r = full[:, 10:15].copy()
+    r[:, 4] = full[:, 30]  # draw kind (written by the draw wave)
+    rts.append(np.concatenate([r, full[:, 28:30]], axis=1))
 
 
 if "--graph" in sys.argv:
@@ -66,6 +71,10 @@ tot = (a.sum(1))
 print(f"f32={f32} waves={nw} steps=200  total cycles median {np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} max {tot.max()}")
 for i, nm in enumerate(names):
     print(f"  {nm:18s} median {np.median(a[:, i]):7.0f}  mean {a[:, i].mean():7.0f}  p90 {np.percentile(a[:, i], 90):7.0f}")
+da = np.concatenate(dacc)
+print(f"draw wave: total cycles median {np.median(da.sum(1)):.0f} p90 {np.percentile(da.sum(1), 90):.0f}")
+for i, nm in enumerate(dnames):
+    print(f"  {nm:18s} median {np.median(da[:, i]):7.0f}  mean {da[:, i].mean():7.0f}  p90 {np.percentile(da[:, i], 90):7.0f}")
 
 # wave placement in time (s_memrealtime, 100 MHz => 10 ns ticks)
 r = np.stack(rts)  # [steps, waves, 4]
@@ -75,6 +84,10 @@ ns = 10.0
 print(f"wave start offset ns: median {np.median(t0)*ns:.0f} p90 {np.percentile(t0, 90)*ns:.0f} max {t0.max(1).mean()*ns:.0f} (mean over steps)")
 print(f"wave end   offset ns: median {np.median(t1)*ns:.0f} p90 {np.percentile(t1, 90)*ns:.0f} max {t1.max(1).mean()*ns:.0f}")
 print(f"wave life ns: median {np.median(t1 - t0)*ns:.0f}")
+d0 = r[:, :, 5] - r[:, :, 0].min(axis=1, keepdims=True)
+d1 = r[:, :, 6] - r[:, :, 0].min(axis=1, keepdims=True)
+print(f"draw wave: start median {np.median(d0)*ns:.0f} ns, end median {np.median(d1)*ns:.0f} p90 {np.percentile(d1, 90)*ns:.0f} "
+      f"max {d1.max(1).mean()*ns:.0f}; ends after its logic wave in {np.mean(d1 > t1)*100:.0f}% of workgroups")
 xcc = r[0, :, 3] & 0xF
 hw = r[0, :, 2]
 cu = (hw >> 8) & 0xF
@@ -104,6 +117,7 @@ kind = r[:, :, 4]  # 1: a lane twisted its MT state, 2: a draw ran past the 8 pr
 for kd, nm in ((0, "plain"), (1, "twist"), (2, "past 8 words"), (3, "both")):
     m = kind == kd
     if m.any():
-        print(f"draw kind {nm:13s}: {m.sum() / len(acc):6.1f} waves/step, draw phase median "
-              f"{np.median(life[:, :, 5][m]):6.0f}, total median {np.median(tot_w[m]):6.0f} cycles")
+        dl = da.reshape(len(dacc), nw, -1)
+        print(f"draw kind {nm:13s}: {m.sum() / len(acc):6.1f} waves/step, draw-wave draws median "
+              f"{np.median(dl[:, :, 4][m]):6.0f}, logic total median {np.median(tot_w[m]):6.0f} cycles")
 print("kind of the slowest wave per step:", np.bincount(kind[np.arange(len(acc)), slow], minlength=4).tolist())
