@@ -184,14 +184,16 @@ int st_state(st_ctx *ctx, st_state_views *out);
  * between the views above and caller buffers (crafted states). */
 int st_copy(void *dst, const void *src, int64_t bytes, st_stream stream);
 
-/* The step kernels keep each env's MT19937 generation double-buffered: the
+/* The step kernels keep each env's MT19937 generation double-buffered (the
  * next generation is computed a few words per draw into a second buffer and
- * becomes current at index 624, so between steps ST_STAT_MT_INDEX carries
- * engine bits above bit 9 and the current words may sit in the second buffer.
- * st_mt_sync (on `stream`) brings every env back to CPython's form: words
- * [0, 624) of its mt row and an index 0..624 equal random.getstate().  Call it
- * before reading stats or mt through st_state's views; st_save calls it
- * itself.  Writing a CPython state (words [0, 624), index 0..624) is always
+ * becomes current at index 624) and draw every env's next piece one spawn
+ * ahead (the "preview", whose words the reference has not consumed yet), so
+ * between steps ST_STAT_MT_INDEX carries engine bits above bit 9 and the
+ * current words may sit in the second buffer.  st_mt_sync (on `stream`)
+ * brings every env back to CPython's form -- words [0, 624) of its mt row and
+ * an index 0..624 equal random.getstate(), the preview's words given back.
+ * Call it before reading stats or mt through st_state's views; st_save calls
+ * it itself.  Writing a CPython state (words [0, 624), index 0..624) is always
  * valid. */
 int st_mt_sync(st_ctx *ctx, st_stream stream);
 
