@@ -450,7 +450,7 @@ def test_mt_generations_across_steps():
         C.check(b._L.st_copy(ctypes.c_void_p(raw.data_ptr()),
                              ctypes.c_void_p(v.stats + C.STAT["mt_index"] * v.stride * 4),
                              raw.numel() * 4, b._stream()))
-        saw_lazy |= bool(((raw[:n].cpu().numpy() >> 20) != 0).any())   # current generation in B
+        saw_lazy |= bool((((raw[:n].cpu().numpy() >> 20) & 1) != 0).any())   # current generation in B
         if (c0 // chunk) % 3 == 1:
             a.get_state(("mt", "stats"))                # sync a only, mid-run
     assert saw_lazy
@@ -460,6 +460,68 @@ def test_mt_generations_across_steps():
     for i in range(n):
         assert int(fa["stats"][13, i]) == ob.envs[i].rng.index, i
         assert np.array_equal(fa["mt"][i], np.ctypeslib.as_array(ob.envs[i].rng.mt)), i
+
+
+def _mt_canonical(words, index):
+    """(words, index) of an MT19937 state with index 624 replaced by the
+    equivalent twisted words and index 0 (CPython twists lazily, at the next
+    draw; the engine may already hold the twisted generation when a rewind
+    lands exactly on a generation boundary).  Same future outputs either way."""
+    mt = np.array(words, dtype=np.uint32)
+    if index < 624:
+        return mt, index
+    w = [int(x) for x in mt]
+    for k in range(624):
+        y = (w[k] & 0x80000000) | (w[(k + 1) % 624] & 0x7FFFFFFF)
+        w[k] = w[(k + 397) % 624] ^ (y >> 1) ^ (0x9908B0DF if y & 1 else 0)
+    return np.array(w, dtype=np.uint32), 0
+
+
+def test_preview_rewind_across_generations():
+    """Each env's next piece is drawn one spawn ahead (the preview, kept in the
+    MT word with the number c of MT words its draw consumed).  A preview whose
+    draw crossed index 624 straddles two generations: st_mt_sync must give its
+    words back into the previous generation's buffer.  Lock every step (hard
+    drops) until such states occur, sync there, compare every env's MT state
+    with CPython's (the oracle), and keep stepping: after a sync the next spawn
+    draws its piece, then a new preview, and the games must not change."""
+    import ctypes
+    from gym_simpletetris_amd import _lib as C
+    G = _engine()
+    n, T = 512, 1600
+    seeds = [7000 + e for e in range(n)]
+    b = G.TetrisBatch(n, autoreset="same_step", seeds=seeds)
+    b.reset()
+    ob = O.OracleBatch(n, seeds)
+    ob.reset()
+    acts = np.full((T, n), 2, np.uint8)              # hard drops: a draw every step
+    acts[::5] = O.splitmix64_actions(11, 0, T, n)[::5]
+    raw = torch.empty(b.stride, dtype=torch.int32, device=b.device)
+    v = b._views
+    syncs, stop = 0, T
+    for t in range(T):
+        if t >= stop:
+            break
+        o, r, _ = b.step(torch.as_tensor(acts[t], device=b.device))
+        ref = ob.rollout(acts[t:t + 1])
+        assert np.array_equal(r.cpu().numpy(), ref["reward"][0]), t
+        assert np.array_equal(o.cpu().numpy().view(np.uint32).T, ref["obs"][0]), t
+        C.check(b._L.st_copy(ctypes.c_void_p(raw.data_ptr()),
+                             ctypes.c_void_p(v.stats + C.STAT["mt_index"] * v.stride * 4),
+                             raw.numel() * 4, b._stream()))
+        w = raw[:n].cpu().numpy().astype(np.uint32)
+        ok = ((w >> 24) & 1).astype(bool)
+        straddle = ok & ((w & 0x3FF) < ((w >> 25) & 63))
+        if straddle.any() and syncs < 3:
+            st = b.get_state(("mt", "stats"))          # st_mt_sync
+            for i in range(n):
+                dev = _mt_canonical(st["mt"][i], int(st["stats"][13, i]))
+                ref = _mt_canonical(np.ctypeslib.as_array(ob.envs[i].rng.mt), ob.envs[i].rng.index)
+                assert dev[1] == ref[1] and np.array_equal(dev[0], ref[0]), (t, i)
+            syncs += 1
+            if syncs == 3:
+                stop = t + 60                            # keep stepping past the last sync
+    assert syncs == 3, "no straddling preview within the run"
 
 
 def _greedy_ref(col_words, W, H, pw):
