@@ -127,11 +127,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uin
 // `nt` stores stream out during the kernel instead (A/B, st_step packed:
 // 6.31 -> 5.89 us with obs, board, counter and MT stores all `nt`).
 constexpr int kNT = 2;
-// A/B knobs: issue priority of the st_step draw wave after B1 (0 = default;
-// rollouts use 2), and which st_step wave builds the next-generation block
-// (1: the logic wave)
+// A/B knobs: issue priority of the draw wave after B1 (its chain is the
+// critical one there: st_step -1.5%, rollouts -6% at 2), and which st_step
+// wave builds the next-generation block (1: the logic wave; measured +1%)
 #ifndef ST_DPRIO
-#define ST_DPRIO 0
+#define ST_DPRIO 2
 #endif
 #ifndef ST_LWORK
 #define ST_LWORK 0
@@ -920,9 +920,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         }
         wg_barrier();  // B1: the draw wave learns which lanes lock
         if constexpr (DO_D) ST_STAMP(10);
-        // the draw wave's chain is the critical one after B1 (rollouts: -6%)
-        constexpr int kDPrio = KSTEPS == 1 ? ST_DPRIO : 2;
-        if constexpr (DO_D && kDPrio > 0) __builtin_amdgcn_s_setprio(kDPrio);
+        if constexpr (DO_D && ST_DPRIO > 0) __builtin_amdgcn_s_setprio(ST_DPRIO);
         if constexpr (DO_D) {
             const uint32_t w = lane < 32 ? sm.lockm[t & 1][0] : sm.lockm[t & 1][1];
             locknow = (w >> (lane & 31)) & 1u;
@@ -964,13 +962,14 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
     // ---------------- logic: lock path (tetris_env.py:263-299) ----------------
     bool died = false, spawn = false;
     int32_t score = 0, lines = 0, holes = 0, height = 0, deaths = 0;
+    int32_t o_score = 0, o_lines = 0, o_holes = 0, o_height = 0, o_deaths = 0;  // (dirty tests)
     uint32_t bdirty = 0;  // st_step: board columns this step changes (stores skip the rest)
     if (DO_L && locknow) {
-        score = (int32_t)ss(ST_STAT_SCORE);
-        lines = (int32_t)ss(ST_STAT_LINES);
-        holes = (int32_t)ss(ST_STAT_HOLES);
-        height = (int32_t)ss(ST_STAT_PIECE_HEIGHT);
-        deaths = (int32_t)ss(ST_STAT_DEATHS);
+        score = o_score = (int32_t)ss(ST_STAT_SCORE);
+        lines = o_lines = (int32_t)ss(ST_STAT_LINES);
+        holes = o_holes = (int32_t)ss(ST_STAT_HOLES);
+        height = o_height = (int32_t)ss(ST_STAT_PIECE_HEIGHT);
+        deaths = o_deaths = (int32_t)ss(ST_STAT_DEATHS);
         paint<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
         // Column words carry the floor bits, so the topmost cell of column v
         // is ctz(v) (H when empty) and its holes are H - ctz(v) - popc(v & hmask):
@@ -1107,7 +1106,18 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
             }
         }
         wave_sync();  // the board reads above precede the overlay paint
-        if (!spawn) paint<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
+        if constexpr (TWO) {
+            // the obs overlay of every lane at once: the current piece, or for
+            // a spawn the preview at the spawn position (known since the step
+            // started); a spawn without a preview gets its piece below, once
+            // the draw wave has drawn it
+            const uint2 pd = tab(pv_id(mt0) * 4);
+            const bool pvs = spawn && pv_ok(mt0);
+            paint<S32>(L, lane, pvs ? pd.x : desc.x, pvs ? pd.y : desc.y, pvs ? W / 2 : ax, pvs ? 0 : ay,
+                       spawn && !pvs ? 0u : hmask);
+        } else {
+            if (!spawn) paint<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
+        }
         if constexpr (LWORK) {
             // next[pg..pg+3] (the draw wave counts it done in the MT word it
             // commits; its own draws treat the block as pending: a finish it
@@ -1238,6 +1248,10 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
             if (__ballot(need1)) {
                 lds_flag_wait(&sm.f2, (uint32_t)t + 1u);
                 if (need1) sid = (int)sm.pick1[lane];
+                if constexpr (KSTEPS == 1) {  // its overlay (the others were painted with the board stores)
+                    const uint2 sd1 = tab(sid * 4);
+                    paint<S32>(L, lane, sd1.x, sd1.y, W / 2, 0, need1 && spawn ? hmask : 0u);
+                }
             }
         }
         ST_STAMP(4);
@@ -1263,15 +1277,15 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         ss(ST_STAT_TIME) = (uint32_t)time;
         ss(kPieceRow) = pw_out;
         if (locknow) {
-            auto put = [&](int r, int32_t v) {
-                if constexpr (KSTEPS == 1) sdirty |= (uint32_t)(ss(r) != (uint32_t)v) << r;
+            auto put = [&](int r, int32_t v, int32_t old) {
+                if constexpr (KSTEPS == 1) sdirty |= (uint32_t)(old != v) << r;
                 ss(r) = (uint32_t)v;
             };
-            put(ST_STAT_SCORE, score);
-            put(ST_STAT_LINES, lines);
-            put(ST_STAT_HOLES, holes);
-            put(ST_STAT_PIECE_HEIGHT, height);
-            put(ST_STAT_DEATHS, deaths);
+            put(ST_STAT_SCORE, score, o_score);
+            put(ST_STAT_LINES, lines, o_lines);
+            put(ST_STAT_HOLES, holes, o_holes);
+            put(ST_STAT_PIECE_HEIGHT, height, o_height);
+            put(ST_STAT_DEATHS, deaths, o_deaths);
         }
         if constexpr (KSTEPS == 1) {
             if constexpr (TWO) sm.SD[lane] = sdirty;
@@ -1279,7 +1293,9 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         }
 
         // ---- observation (tetris_env.py:301-302): board + current piece ----
-        if (KSTEPS != 1 || spawn) paint<S32>(L, lane, odesc.x, odesc.y, oax, oay, hmask);
+        if constexpr (!(KSTEPS == 1 && TWO)) {
+            if (KSTEPS != 1 || spawn) paint<S32>(L, lane, odesc.x, odesc.y, oax, oay, hmask);
+        }
         wave_sync();
         const bool wide_obs = (p.n & 3) == 0 && e0 + kWave <= p.n &&
                               (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0;
