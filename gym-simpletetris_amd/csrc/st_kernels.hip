@@ -1004,13 +1004,39 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
             ncl = __builtin_popcount(andv);
             orv = 0;
             sctz = spop = 0;
+            if constexpr (WT != 0) {
+                // the columns in registers, one full row per round for all of
+                // them (compact()'s steps in the same order): the rounds are
+                // the wave's largest clear count, not one loop per column
+                uint32_t c[WT];
+#pragma unroll
+                for (int x = 0; x < WT; ++x) c[x] = lcol(L, x, lane) & hmask;
+                uint32_t full = andv;
+                while (full) {
+                    const int r = __builtin_ctz(full);
+                    full &= full - 1u;
+                    const uint32_t above = (1u << r) - 1u;
+                    const uint32_t keep = ~(above | (1u << r));
+#pragma unroll
+                    for (int x = 0; x < WT; ++x) c[x] = (c[x] & keep) | ((c[x] & above) << 1);
+                }
+#pragma unroll
+                for (int x = 0; x < WT; ++x) {
+                    const uint32_t v = c[x] | floorb;
+                    lcol(L, x, lane) = v;
+                    orv |= v;
+                    sctz += __builtin_ctz(v);
+                    spop += __builtin_popcount(v);
+                }
+            } else {
 #pragma unroll 8
-            for (int x = 0; x < W; ++x) {
-                const uint32_t v = compact(lcol(L, x, lane) & hmask, andv) | floorb;
-                lcol(L, x, lane) = v;
-                orv |= v;
-                sctz += __builtin_ctz(v);
-                spop += __builtin_popcount(v);
+                for (int x = 0; x < W; ++x) {
+                    const uint32_t v = compact(lcol(L, x, lane) & hmask, andv) | floorb;
+                    lcol(L, x, lane) = v;
+                    orv |= v;
+                    sctz += __builtin_ctz(v);
+                    spop += __builtin_popcount(v);
+                }
             }
             lines += ncl;
         }
