@@ -1553,9 +1553,9 @@ __global__ __launch_bounds__(kWave) void k_reset(KParams p) {
 }
 
 // ---------------------------------------------------------------- seed
-// random.seed(s): init_by_array(key = 32-bit limbs of s) (+ the first twist,
-// done here so the step kernels start at index 0), and the counter values of
-// TetrisEngine.__init__ (:165-181).  One lane per env, serial (one-time).
+// random.seed(s): init_by_array(key = 32-bit limbs of s) (+ the first twist
+// into the second buffer), and the counter values of TetrisEngine.__init__
+// (:165-181).  One lane per env, serial (one-time).
 __global__ void k_seed(KParams p) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= p.stride) return;
@@ -1594,18 +1594,23 @@ __global__ void k_seed(KParams p) {
         }
     }
     g[0] = 0x80000000u;
-    // first twist (genrand_uint32 with index == N)
+    // A now holds CPython's state after random.seed (index 624: the first
+    // draw twists).  The first twist goes to B as the complete next
+    // generation (genrand_uint32 with index == N, out of place), so the
+    // first draw switches to it like any other generation end, and
+    // st_mt_sync of a fresh context returns exactly random.getstate().
+    uint32_t *nx = g + kMtB;
     int kk = 0;
-    for (; kk < kMtN - 397; ++kk) g[kk] = g[kk + 397] ^ mt_mix(g[kk], g[kk + 1]);
-    for (; kk < kMtN - 1; ++kk) g[kk] = g[kk + (397 - kMtN)] ^ mt_mix(g[kk], g[kk + 1]);
-    g[kMtN - 1] = g[396] ^ mt_mix(g[kMtN - 1], g[0]);
+    for (; kk < kMtN - 397; ++kk) nx[kk] = g[kk + 397] ^ mt_mix(g[kk], g[kk + 1]);
+    for (; kk < kMtN - 1; ++kk) nx[kk] = nx[kk + (397 - kMtN)] ^ mt_mix(g[kk], g[kk + 1]);
+    nx[kMtN - 1] = nx[396] ^ mt_mix(g[kMtN - 1], nx[0]);
 
     const int64_t sd = p.stride;
     int32_t *st = p.stats + e;
     for (int r = 0; r < ST_NSTAT; ++r) st[r * sd] = 0;
     st[ST_STAT_TIME * sd] = -1;   // :165
     st[ST_STAT_SCORE * sd] = -1;  // :166
-    st[ST_STAT_MT_INDEX * sd] = 0;
+    st[ST_STAT_MT_INDEX * sd] = (int32_t)mt_pack(kMtN, kMtN, 0);  // index 624, next generation complete
     for (int x = 0; x < p.W; ++x) p.board[x * sd + e] = 0u;
     p.piece[e] = pack_piece(0, 0, p.W / 2, 0, 0);
 }
@@ -1629,8 +1634,14 @@ __global__ __launch_bounds__(kWave) void k_mt_sync(KParams p) {
     int idx = (int)(r & 0x3FFu);
     uint32_t cur = (r >> 20) & 1u;
     if (pv_ok(r)) {
+        // A preview draw always starts where an earlier draw ended (index
+        // >= 1 of its generation), so idx > c: it stayed in one generation;
+        // idx <= c: it started at index 624 - (c - idx) of the previous one,
+        // which is intact (nothing is built into it while the preview is
+        // pending).  idx == c is a draw that started exactly at 624: CPython
+        // holds the old words with index 624 (it twists lazily).
         const int c = (int)((r >> 25) & kPvCMax);
-        if (idx >= c) {
+        if (idx > c) {
             idx -= c;
         } else {
             idx = kMtN - (c - idx);

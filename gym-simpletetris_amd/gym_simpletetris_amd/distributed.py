@@ -80,16 +80,9 @@ class ShardedTetris:
         self.engine.reset()
 
     def step(self, actions: torch.Tensor):
-        """Step the shard, writing straight into the gather buffer."""
-        from . import _lib as C
-        import ctypes
-        e = self.engine
-        with torch.cuda.device(e.device):
-            C.check(e._L.st_step(e._ctx, ctypes.c_void_p(actions.data_ptr()),
-                                 ctypes.c_void_p(self._obs.data_ptr()),
-                                 ctypes.c_void_p(self._rew.data_ptr()),
-                                 ctypes.c_void_p(self._done.data_ptr()), e._stream()))
-        return self._obs, self._rew, self._done
+        """Step the shard, writing straight into the gather buffer (the
+        engine's own action checks apply: shape, dtype, device, 0..6)."""
+        return self.engine.step(actions, obs="packed", out=(self._obs, self._rew, self._done))
 
     def gather(self, dst: int = 0, cpu: bool = False):
         """RCCL gather of the packed outputs to `dst` (cpu=True: via host

@@ -42,7 +42,8 @@ class TetrisBatch:
                  penalise_height: bool = False, penalise_height_increase: bool = False,
                  advanced_clears: bool = False, high_scoring: bool = False,
                  penalise_holes: bool = False, penalise_holes_increase: bool = False,
-                 autoreset: str = "none", device=None, seeds: Optional[Sequence[int]] = None):
+                 autoreset: str = "none", device=None, seeds: Optional[Sequence[int]] = None,
+                 validate_actions: bool = True):
         self._L = C.load()
         if not torch.cuda.is_available():
             raise RuntimeError("TetrisBatch needs a ROCm GPU (no CPU fallback by design)")
@@ -71,6 +72,11 @@ class TetrisBatch:
         self.kwargs = dict(kw, lock_delay=self.lock_delay, width=self.width, height=self.height)
         self.autoreset = autoreset
         self.device = device
+        # step()/rollout() reject actions outside 0..6 like the reference's
+        # value_action_map[action] KeyError (tetris_env.py:245).  For a device
+        # tensor that check costs one device->host sync per call;
+        # validate_actions=False skips it (values >= 7 then act as idle).
+        self.validate_actions = bool(validate_actions)
         cfg = C.Config(self.width, self.height, self.lock_delay, flags, C.AUTORESET[autoreset])
         ctx = ctypes.c_void_p()
         with torch.cuda.device(device):
@@ -130,6 +136,35 @@ class TetrisBatch:
             raise ValueError(f"{name} must have {self.n} entries, got {t.numel()}")
         return t.contiguous()
 
+    def _actions(self, x, lead=()) -> torch.Tensor:
+        """Actions as a contiguous uint8 device tensor of shape lead + (n,),
+        range-checked BEFORE the cast (a cast would wrap -1 to 255 and 263 to
+        7): the reference raises KeyError for an action outside
+        value_action_map (tetris_env.py:152-160, :245)."""
+        shape = tuple(lead) + (self.n,)
+        if isinstance(x, torch.Tensor):
+            if x.dtype.is_floating_point or x.dtype == torch.bool or x.is_complex():
+                raise TypeError(f"actions must be integers, got {x.dtype}")
+            if tuple(x.shape) != shape and x.numel() != int(np.prod(shape)):
+                raise ValueError(f"actions must have shape {shape}, got {tuple(x.shape)}")
+            if self.validate_actions or x.device != self.device:
+                bad = (x < 0) | (x > 6) if x.dtype != torch.uint8 else (x > 6)
+                if bool(bad.any()):
+                    v = x[bad].flatten()[0].item()
+                    raise KeyError(f"action {v} not in 0..6 (tetris_env.py:245)")
+            t = x if (x.dtype == torch.uint8 and x.device == self.device) \
+                else x.to(device=self.device, dtype=torch.uint8)
+            return t.reshape(shape).contiguous()
+        a = np.asarray(x)
+        if a.dtype.kind not in "iub":
+            a = a.astype(np.int64)
+        if a.size != int(np.prod(shape)):
+            raise ValueError(f"actions must have shape {shape}, got {a.shape}")
+        if a.size and (int(a.min()) < 0 or int(a.max()) > 6):
+            v = a.flat[np.flatnonzero((a < 0) | (a > 6))[0]]
+            raise KeyError(f"action {v} not in 0..6 (tetris_env.py:245)")
+        return torch.as_tensor(a.astype(np.uint8).reshape(shape), device=self.device)
+
     def reset(self, mask=None):
         """TetrisEngine.clear() on every env (mask None) or where mask != 0."""
         if not self._seeded:
@@ -138,25 +173,36 @@ class TetrisBatch:
         with torch.cuda.device(self.device):
             C.check(self._L.st_reset(self._ctx, _ptr(m), self._stream()))
 
-    def step(self, actions, obs: str = "packed"):
+    def step(self, actions, obs: str = "packed", out=None):
         """One TetrisEngine.step on every env.  obs: 'packed' (u32 [W][n]),
         'f32' (also float32 [n][W][H], fused in the kernel) or 'none'.
-        Returns (obs, reward int32 [n], done bool [n]) -- reused buffers."""
-        a = actions if (isinstance(actions, torch.Tensor) and actions.dtype == torch.uint8
-                        and actions.device == self.device and actions.is_contiguous()) \
-            else self._as_dev_u8(actions, "actions")
+        Returns (obs, reward int32 [n], done bool [n]) -- reused buffers, or
+        the caller's `out` = (packed obs int32 [W][n], reward int32 [n],
+        done uint8/bool [n]) device tensors (e.g. a gather buffer's views)."""
+        if obs not in ("packed", "f32", "none"):
+            raise ValueError("obs must be 'packed', 'f32' or 'none'")
+        a = self._actions(actions)
+        o_t, r_t, d_t = (self.obs, self.reward, self.done) if out is None else out
+        if out is not None:
+            for t, dt, shape in ((o_t, torch.int32, (self.width, self.n)),
+                                 (r_t, torch.int32, (self.n,)), (d_t, None, (self.n,))):
+                if t.device != self.device or tuple(t.shape) != shape or not t.is_contiguous() \
+                        or (dt is not None and t.dtype != dt) \
+                        or (dt is None and t.dtype not in (torch.uint8, torch.bool)):
+                    raise ValueError(f"out tensor {tuple(t.shape)} {t.dtype} on {t.device}: "
+                                     f"need contiguous {shape} on {self.device}")
         s = self._stream()
         with torch.cuda.device(self.device):
             if obs == "f32":
                 if self.obs_f32 is None:
                     self.obs_f32 = torch.zeros((self.n, self.width, self.height),
                                                dtype=torch.float32, device=self.device)
-                C.check(self._L.st_step_f32(self._ctx, _ptr(a), _ptr(self.obs), _ptr(self.obs_f32),
-                                            _ptr(self.reward), _ptr(self.done), s))
-                return self.obs_f32, self.reward, self.done
-            C.check(self._L.st_step(self._ctx, _ptr(a), _ptr(self.obs) if obs == "packed" else None,
-                                    _ptr(self.reward), _ptr(self.done), s))
-        return (self.obs if obs == "packed" else None), self.reward, self.done
+                C.check(self._L.st_step_f32(self._ctx, _ptr(a), _ptr(o_t), _ptr(self.obs_f32),
+                                            _ptr(r_t), _ptr(d_t), s))
+                return self.obs_f32, r_t, d_t
+            C.check(self._L.st_step(self._ctx, _ptr(a), _ptr(o_t) if obs == "packed" else None,
+                                    _ptr(r_t), _ptr(d_t), s))
+        return (o_t if obs == "packed" else None), r_t, d_t
 
     def rollout(self, actions: torch.Tensor, obs: str = "packed", out: Optional[dict] = None):
         """K consecutive steps in one kernel launch (st_rollout).
@@ -166,10 +212,11 @@ class TetrisBatch:
         [K, n, W, H] ('f32') or None ('none'); reward int32 [K, n]; done bool
         [K, n].  Identical to K calls of step().  `out` may supply the output
         tensors (keys 'obs', 'obs_f32', 'reward', 'done') to reuse buffers."""
-        if actions.dtype != torch.uint8 or actions.device != self.device or actions.dim() != 2 \
-                or actions.shape[1] != self.n or not actions.is_contiguous():
-            raise ValueError(f"actions must be a contiguous uint8 [K, {self.n}] tensor on {self.device}")
+        if not isinstance(actions, torch.Tensor) or actions.dim() != 2 or actions.shape[1] != self.n \
+                or actions.shape[0] < 1:
+            raise ValueError(f"actions must be a [K, {self.n}] integer tensor")
         K = int(actions.shape[0])
+        actions = self._actions(actions, lead=(K,))
         out = {} if out is None else out
         W, H, n, dev = self.width, self.height, self.n, self.device
 
@@ -304,9 +351,12 @@ class TetrisBatch:
             C.check(self._L.st_render(self._ctx, _ptr(out), self._stream()))
         return out
 
-    def info_tensors(self) -> dict:
-        """get_info() (tetris_env.py:232-241) for every env as int32 device tensors."""
-        st = self.state_tensors(("stats",), sync=False)["stats"][:, : self.n]
+    def info_tensors(self, stats: Optional[torch.Tensor] = None) -> dict:
+        """get_info() (tetris_env.py:232-241) for every env as int32 device
+        tensors, from the live state or a `stats` snapshot of it."""
+        if stats is None:
+            stats = self.state_tensors(("stats",), sync=False)["stats"]
+        st = stats[:, : self.n]
         return dict(time=st[C.STAT["time"]], score=st[C.STAT["score"]],
                     lines_cleared=st[C.STAT["lines"]], holes=st[C.STAT["holes"]],
                     deaths=st[C.STAT["deaths"]], piece_height=st[C.STAT["piece_height"]],

@@ -64,7 +64,8 @@ class TetrisEnv:
                                   advanced_clears=advanced_clears, high_scoring=high_scoring,
                                   penalise_holes=penalise_holes,
                                   penalise_holes_increase=penalise_holes_increase,
-                                  autoreset="none", device=device)
+                                  autoreset="none", device=device,
+                                  validate_actions=False)  # step() checks the action itself
         self._rng_mode = rng
         self.engine.seed([0 if seed is None else seed])
         if rng == "global" and seed is not None:
@@ -230,16 +231,19 @@ class TetrisEnv:
 
 
 class VecInfo:
-    """Lazy get_info() for N envs: counters are read from the device state
-    only when a key is accessed (int32 tensors on the GPU)."""
+    """get_info() (tetris_env.py:232-241) for N envs as int32 GPU tensors.
+    The counters are snapshotted (one device-to-device copy on the step's
+    stream) when step() returns, so an info kept past later steps still
+    describes its own step; the per-key tensors are built on first access."""
 
     def __init__(self, engine: TetrisBatch):
         self._engine = engine
+        self._stats = engine.state_tensors(("stats",), sync=False)["stats"]
         self._cache = None
 
     def _load(self):
         if self._cache is None:
-            self._cache = self._engine.info_tensors()
+            self._cache = self._engine.info_tensors(self._stats)
         return self._cache
 
     def __getitem__(self, k):

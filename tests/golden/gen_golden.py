@@ -19,6 +19,8 @@ Fixtures:
   greedy.npz           F2  greedy-placement rollouts (1-4 line clears)
   crafted.npz          F3  crafted known-answer cases per reference rule
   grayscale.npz        F5  convert_grayscale images (next row, R19)
+  render.npz           F5b engine.render(), render("rgb_array") and grayscale/rgb obs
+                           along uniform-action games (python gen_golden.py render)
 
 Usage: python tests/golden/gen_golden.py  (writes next to this file)
 """
@@ -419,11 +421,74 @@ def gen_grayscale():
                         g160=np.array(g160, np.uint8))
 
 
-def main():
+# ---------------------------------------------------------------- F5b
+RENDER_RUNS = (("default", dict(), 4242), ("small_odd", dict(width=7, height=12), 4343),
+               ("tall_wide", dict(width=13, height=26), 4444))
+RENDER_AT = (0, 3, 11, 40, 77, 120, 199)
+
+
+def gen_render():
+    """engine.render() (tetris_env.py:317-321), env.render('rgb_array')
+    (:458-462) and the 'grayscale' / 'rgb' observations (:413-433) along
+    uniform-action games: one env per obs_type, same seed and actions, so the
+    three runs see the same boards."""
+    blob, meta = {}, {}
+    steps = max(RENDER_AT) + 1
+    for name, cfg, seed in RENDER_RUNS:
+        acts = splitmix64_actions(0xBEEF, 0, steps, 1)[:, 0]
+        envs = {}
+        states = {}
+        for ot in ("ram", "grayscale", "rgb"):
+            envs[ot] = ref.TetrisEnv(obs_type=ot, **cfg)
+            random.seed(seed)
+            o = envs[ot].reset()
+            states[ot] = random.getstate()
+        packed, rgb, gray, rgbobs = [], [], [], []
+        for t in range(steps):
+            obs = {}
+            for ot, env in envs.items():
+                random.setstate(states[ot])
+                o, r, d, info = env.step(int(acts[t]))
+                obs[ot] = o
+                if d:
+                    env.reset()
+                states[ot] = random.getstate()
+            if t in RENDER_AT:
+                e = envs["ram"]
+                packed.append(pack_cols(e.engine.render()))
+                img = e.render("rgb_array")
+                assert img.dtype == np.uint8 and img.shape == (160, 160, 3)
+                assert (img == img[:, :, :1]).all()
+                rgb.append(img[:, :, 0])
+                g = obs["grayscale"]
+                assert g.dtype == np.float32 and g.shape == (84, 84)
+                gray.append(g.astype(np.uint8))
+                c = obs["rgb"]
+                assert c.shape == (84, 84, 3) and (c == c[:, :, :1]).all()
+                assert np.array_equal(c[:, :, 0], g)
+                rgbobs.append(c[:, :, 0].astype(np.uint8))
+        blob[f"{name}/actions"] = acts.astype(np.uint8)
+        blob[f"{name}/render"] = np.array(packed, np.uint32)
+        blob[f"{name}/rgb160"] = np.array(rgb, np.uint8)
+        blob[f"{name}/gray84"] = np.array(gray, np.uint8)
+        meta[name] = dict(cfg=cfg, seed=seed, at=list(RENDER_AT))
+        print("render", name, len(packed), "frames")
+    blob["meta"] = np.array(json.dumps(meta))
+    np.savez_compressed(os.path.join(HERE, "render.npz"), **blob)
+
+
+GENERATORS = ("mt", "crafted", "rollouts", "greedy", "grayscale", "render")
+
+
+def main(which=GENERATORS):
     global ref
     if not os.path.exists(REF):
         raise SystemExit("reference not present; fixtures are committed, nothing to do")
     ref = load_reference()
+    if "render" in which:
+        gen_render()
+    if not set(which) - {"render"}:
+        return
     gen_mt()
     gen_crafted()
     save_rollout_set("rollouts.npz", "uniform", 16, 400, list(CONFIGS))
@@ -434,4 +499,6 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    # no arguments: every fixture; else a subset of GENERATORS (only "render"
+    # is generated on its own, the others are written together)
+    main(tuple(sys.argv[1:]) or GENERATORS)

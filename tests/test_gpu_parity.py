@@ -15,6 +15,7 @@ pytestmark = pytest.mark.gpu
 ROLL = load_set("rollouts.npz")
 GREEDY = load_set("greedy.npz")
 CRAFTED = load_set("crafted.npz")
+RENDER = load_set("render.npz")
 
 
 def _engine():
@@ -72,13 +73,25 @@ def test_library_is_the_hip_build():
     torch.cuda.synchronize()
 
 
+def _twist(words):
+    """One MT19937 generation refill (CPython genrand_uint32 at index 624)."""
+    w = [int(x) for x in words]
+    for k in range(624):
+        y = (w[k] & 0x80000000) | (w[(k + 1) % 624] & 0x7FFFFFFF)
+        w[k] = w[(k + 397) % 624] ^ (y >> 1) ^ (0x9908B0DF if y & 1 else 0)
+    return np.array(w, dtype=np.uint32)
+
+
 def test_device_mt19937_matches_cpython():
-    """Seed kernel (init_by_array + first twist) == CPython's first 624 outputs."""
+    """Seed kernel (init_by_array) == random.Random(seed).getstate() exactly
+    (words and index 624), and its first generation == CPython's first 624
+    outputs."""
     G = _engine()
     d = np.load(f"{GOLDEN}/mt19937.npz")
     seeds = [int(s) for s in d["seeds"]]
-    b = G.TetrisBatch(len(seeds), seeds=seeds)
-    mt = b.get_state(("mt",))["mt"]
+    b = G.TetrisBatch(len(seeds), seeds=seeds, autoreset="same_step")
+    st = b.get_state(("mt", "stats"))
+    mt = st["mt"]
 
     def temper(y):
         y = y ^ (y >> np.uint32(11))
@@ -86,8 +99,24 @@ def test_device_mt19937_matches_cpython():
         y = y ^ ((y << np.uint32(15)) & np.uint32(0xEFC60000))
         return y ^ (y >> np.uint32(18))
 
+    for i, s in enumerate(seeds):
+        cp = random.Random(s).getstate()[1]
+        assert np.array_equal(mt[i], np.array(cp[:624], np.uint32)), f"seed {s}"
+        assert int(st["stats"][13, i]) == cp[624] == 624
+        assert np.array_equal(temper(_twist(mt[i])), d["words"][i][:624]), f"seed {s}"
+    # and the engine draws from it: reset + a few steps against the oracle
+    b.reset()
+    ob = O.OracleBatch(len(seeds), seeds)
+    ob.reset()
+    acts = np.full((30, len(seeds)), 2, np.uint8)
+    ref = ob.rollout(acts)
+    for t in range(30):
+        obs, rew, done = b.step(torch.as_tensor(acts[t], device=b.device))
+        assert np.array_equal(obs.cpu().numpy().view(np.uint32).T, ref["obs"][t]), t
+    fin = b.get_state(("mt", "stats"))
     for i in range(len(seeds)):
-        assert np.array_equal(temper(mt[i]), d["words"][i][:624]), f"seed {seeds[i]}"
+        assert int(fin["stats"][13, i]) == ob.envs[i].rng.index
+        assert np.array_equal(fin["mt"][i], np.ctypeslib.as_array(ob.envs[i].rng.mt))
 
 
 @pytest.mark.parametrize("name", sorted(CRAFTED))
@@ -286,6 +315,45 @@ def test_single_env_errors_and_render():
     assert o.shape == (84, 84, 3)
 
 
+@pytest.mark.parametrize("name", sorted(RENDER))
+def test_render_and_image_obs_vs_reference(name):
+    """render_packed() (engine.render(), tetris_env.py:317-321), the
+    160x160x3 render('rgb_array') frame (:458-462) and the 'grayscale' /
+    'rgb' observations (:413-433) bit for bit against the reference's own
+    outputs along the same games (tests/golden/render.npz)."""
+    G = _engine()
+    meta, arrs = RENDER[name]
+    envs = {ot: G.TetrisEnv(obs_type=ot, rng="private", seed=meta["seed"], **meta["cfg"])
+            for ot in ("ram", "grayscale", "rgb")}
+    for env in envs.values():
+        env.reset()
+    k = 0
+    for t, a in enumerate(arrs["actions"]):
+        obs = {}
+        for ot, env in envs.items():
+            o, r, d, info = env.step(int(a))
+            obs[ot] = o
+            if d:
+                env.reset()
+        if t in meta["at"]:
+            e = envs["ram"]
+            packed = e.engine.render_packed().cpu().numpy().view(np.uint32)[:, 0]
+            assert np.array_equal(packed, arrs["render"][k]), (name, t)
+            img = e.render("rgb_array")
+            assert img.dtype == np.uint8 and img.shape == (160, 160, 3)
+            assert np.array_equal(img, np.repeat(arrs["rgb160"][k][:, :, None], 3, axis=2)), (name, t)
+            g = obs["grayscale"]
+            assert g.dtype == np.float32 and g.shape == (84, 84)
+            assert np.array_equal(g, arrs["gray84"][k].astype(np.float32)), (name, t)
+            c = obs["rgb"]
+            assert c.dtype == np.float32 and c.shape == (84, 84, 3)
+            assert np.array_equal(c, np.repeat(arrs["gray84"][k][:, :, None], 3, axis=2).astype(np.float32))
+            k += 1
+    assert k == len(meta["at"])
+    for env in envs.values():
+        env.close()
+
+
 def test_vec_env_surface():
     G = _engine()
     v = G.make("SimpleTetrisVec-v0", num_envs=256, seed=11, advanced_clears=True)
@@ -296,6 +364,14 @@ def test_vec_env_surface():
         assert o.shape == (256, 10, 20) and r.dtype == torch.int32 and d.dtype == torch.bool
     assert info["time"].shape == (256,)
     assert int(info["deaths"].sum()) > 0
+    # an info kept past later steps still describes its own step
+    kept = v.step(torch.zeros(256, dtype=torch.uint8, device=v.device))[3]
+    live = {k: x.clone() for k, x in v.engine.info_tensors().items()}   # the state right now
+    for _ in range(3):
+        v.step(torch.full((256,), 2, dtype=torch.uint8, device=v.device))
+    for k in ("time", "score", "holes", "deaths", "ep_time", "statistics"):
+        assert torch.equal(kept[k], live[k]), k
+    assert not torch.equal(v.engine.info_tensors()["time"], live["time"])
 
 
 @pytest.mark.parametrize("autoreset", ["same_step", "none"])
@@ -462,19 +538,54 @@ def test_mt_generations_across_steps():
         assert np.array_equal(fa["mt"][i], np.ctypeslib.as_array(ob.envs[i].rng.mt)), i
 
 
-def _mt_canonical(words, index):
-    """(words, index) of an MT19937 state with index 624 replaced by the
-    equivalent twisted words and index 0 (CPython twists lazily, at the next
-    draw; the engine may already hold the twisted generation when a rewind
-    lands exactly on a generation boundary).  Same future outputs either way."""
-    mt = np.array(words, dtype=np.uint32)
-    if index < 624:
-        return mt, index
-    w = [int(x) for x in mt]
-    for k in range(624):
-        y = (w[k] & 0x80000000) | (w[(k + 1) % 624] & 0x7FFFFFFF)
-        w[k] = w[(k + 397) % 624] ^ (y >> 1) ^ (0x9908B0DF if y & 1 else 0)
-    return np.array(w, dtype=np.uint32), 0
+@pytest.mark.parametrize("mode", ["step", "rollout"])
+def test_sync_at_generation_boundary(mode):
+    """A spawn whose draw takes the generation's last word (index 623) leaves
+    CPython at index 624 with the OLD words (it twists lazily); the preview
+    drawn right after it starts at 624 and runs into the next generation.
+    st_mt_sync must give back exactly (old words, 624), and stepping on from
+    the synced state must match the oracle."""
+    G = _engine()
+    n = 64
+    b = G.TetrisBatch(n, autoreset="same_step", seeds=range(100, 100 + n))
+    b.reset()
+    ob = O.OracleBatch(n, list(range(100, 100 + n)))
+    ob.reset()
+    st = b.get_state(("mt", "stats"))
+    mt, stats = st["mt"].copy(), st["stats"].copy()
+    acc = _untemper(0)                  # accepted by any randint range
+    for i in range(n):
+        mt[i, 623] = acc
+        stats[13, i] = 623
+        e = ob.envs[i]
+        for k in range(624):
+            e.rng.mt[k] = int(mt[i, k])
+        e.rng.index = 623
+    b.set_state(mt=mt, stats=stats)
+    acts = np.full((1, n), 2, np.uint8)  # hard drop: every env locks and spawns
+    ref = ob.rollout(acts)
+    if mode == "step":
+        obs, rew, _ = b.step(torch.as_tensor(acts[0], device=b.device))
+        assert np.array_equal(rew.cpu().numpy(), ref["reward"][0])
+    else:
+        obs, rew, _ = b.rollout(torch.as_tensor(acts, device=b.device))
+        assert np.array_equal(rew.cpu().numpy(), ref["reward"])
+    fin = b.get_state(("mt", "stats"))
+    for i in range(n):
+        assert ob.envs[i].rng.index == 624
+        assert int(fin["stats"][13, i]) == 624, i
+        assert np.array_equal(fin["mt"][i], mt[i]), i          # the old generation's words
+    acts = O.splitmix64_actions(8, 0, 80, n)
+    acts[::2] = 2
+    ref = ob.rollout(acts)
+    for t in range(80):
+        obs, rew, _ = b.step(torch.as_tensor(acts[t], device=b.device))
+        assert np.array_equal(rew.cpu().numpy(), ref["reward"][t]), t
+        assert np.array_equal(obs.cpu().numpy().view(np.uint32).T, ref["obs"][t]), t
+    fin = b.get_state(("mt", "stats"))
+    for i in range(n):
+        assert int(fin["stats"][13, i]) == ob.envs[i].rng.index, i
+        assert np.array_equal(fin["mt"][i], np.ctypeslib.as_array(ob.envs[i].rng.mt)), i
 
 
 def test_preview_rewind_across_generations():
@@ -498,7 +609,7 @@ def test_preview_rewind_across_generations():
     acts[::5] = O.splitmix64_actions(11, 0, T, n)[::5]
     raw = torch.empty(b.stride, dtype=torch.int32, device=b.device)
     v = b._views
-    syncs, stop = 0, T
+    syncs, stop, boundary = 0, T, 0
     for t in range(T):
         if t >= stop:
             break
@@ -514,10 +625,10 @@ def test_preview_rewind_across_generations():
         straddle = ok & ((w & 0x3FF) < ((w >> 25) & 63))
         if straddle.any() and syncs < 3:
             st = b.get_state(("mt", "stats"))          # st_mt_sync
-            for i in range(n):
-                dev = _mt_canonical(st["mt"][i], int(st["stats"][13, i]))
-                ref = _mt_canonical(np.ctypeslib.as_array(ob.envs[i].rng.mt), ob.envs[i].rng.index)
-                assert dev[1] == ref[1] and np.array_equal(dev[0], ref[0]), (t, i)
+            for i in range(n):  # exactly random.getstate(): words and index (624 included)
+                assert int(st["stats"][13, i]) == ob.envs[i].rng.index, (t, i)
+                assert np.array_equal(st["mt"][i], np.ctypeslib.as_array(ob.envs[i].rng.mt)), (t, i)
+                boundary += int(st["stats"][13, i]) == 624
             syncs += 1
             if syncs == 3:
                 stop = t + 60                            # keep stepping past the last sync
@@ -583,6 +694,7 @@ def test_greedy_policy_and_clear_heavy_parity():
     b = G.TetrisBatch(n, autoreset="same_step", seeds=seeds, **kw)
     b.reset()
     acts = np.zeros((T, n), np.uint8)
+    got = []
     for t in range(T):
         if t % 40 == 7:  # the policy itself, explore off, vs numpy
             a0 = b.policy_greedy(t, seed=3, explore=0).cpu().numpy().copy()
@@ -591,10 +703,18 @@ def test_greedy_policy_and_clear_heavy_parity():
                 assert int(a0[e]) == _greedy_ref(st["board"][:, e], W, H, int(st["piece"][e])), (t, e)
         a = b.policy_greedy(t, seed=3, explore=30)
         acts[t] = a.cpu().numpy()
-        b.step(a)
+        o, r, d = b.step(a)
+        got.append((o.cpu().numpy().view(np.uint32).T.copy(), r.cpu().numpy().copy(),
+                    d.cpu().numpy().astype(np.uint8)))
     ob = O.OracleBatch(n, seeds, **kw)
     ob.reset()
     ref = ob.rollout(acts)
+    # st_step on the clear-heavy trajectory (its line clears with the preview
+    # and draw wave live; get_state above syncs only every 40 steps)
+    for t in range(T):
+        assert np.array_equal(got[t][1], ref["reward"][t]), t
+        assert np.array_equal(got[t][2], ref["done"][t]), t
+        assert np.array_equal(got[t][0], ref["obs"][t]), t
     c = G.TetrisBatch(n, autoreset="same_step", seeds=seeds, **kw)
     c.reset()
     obs, rew, done = c.rollout(torch.as_tensor(acts, device=c.device))
@@ -654,6 +774,33 @@ def test_wrapper_validation():
         b.rollout(torch.zeros((3, 9), dtype=torch.uint8, device=b.device))
     with pytest.raises(ValueError):
         G.TetrisBatch(4, autoreset="sometimes")
+    # actions outside value_action_map raise like the reference's KeyError
+    # (tetris_env.py:245), before any uint8 cast could wrap them
+    for bad in (np.full(10, 7), np.full(10, -1), np.full(10, 263)):
+        with pytest.raises(KeyError):
+            b.step(bad)
+        with pytest.raises(KeyError):
+            b.step(torch.as_tensor(bad, device=b.device))
+    with pytest.raises(KeyError):
+        b.step(torch.full((10,), 7, dtype=torch.uint8, device=b.device))
+    with pytest.raises(KeyError):
+        b.rollout(torch.full((3, 10), -1, dtype=torch.int64, device=b.device))
+    with pytest.raises(TypeError):
+        b.step(torch.zeros(10, dtype=torch.float32, device=b.device))
+    before = b.get_state()
+    after = b.get_state()
+    for k in before:  # rejected calls did not step
+        assert np.array_equal(before[k], after[k])
+    b.step(torch.arange(10, device=b.device) % 7)     # int64 device actions in range
+    from gym_simpletetris_amd.distributed import ShardedTetris
+    sh = ShardedTetris(20, seed=5, rank=1, world=2, device=b.device)
+    sh.reset()
+    with pytest.raises(KeyError):
+        sh.step(torch.full((10,), 9, dtype=torch.uint8, device=b.device))
+    with pytest.raises(ValueError):
+        sh.step(torch.zeros(11, dtype=torch.uint8, device=b.device))
+    o, r, d = sh.step(torch.zeros(10, dtype=torch.uint8, device=b.device))
+    assert o.data_ptr() == sh.buf.data_ptr()
 
 
 def test_save_load_snapshot(tmp_path):
