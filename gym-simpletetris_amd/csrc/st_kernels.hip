@@ -127,14 +127,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uin
 // `nt` stores stream out during the kernel instead (A/B, st_step packed:
 // 6.31 -> 5.89 us with obs, board, counter and MT stores all `nt`).
 constexpr int kNT = 2;
-// A/B knobs: issue priority of the draw wave after B1 (its chain is the
-// critical one there: st_step -1.5%, rollouts -6% at 2), and which st_step
-// wave builds the next-generation block (1: the logic wave; measured +1%)
+// A/B knob: issue priority of the draw wave after B1 (its chain is the
+// critical one there: st_step -1.5%, rollouts -6% at 2)
 #ifndef ST_DPRIO
 #define ST_DPRIO 2
 #endif
-#ifndef ST_LWORK
-#define ST_LWORK 0
+#ifndef ST_LPRIO
+#define ST_LPRIO 0
 #endif
 template <int AUX = 0>
 __device__ __forceinline__ void buf_store16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
@@ -245,14 +244,20 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
 //   new[623] = new[396] ^ mix(old[623], new[0]).
 // Each env keeps two generation buffers A and B (kMtPitch words: A[624] B[624]
 // pad[16]).  Draws read the current one; the next generation is computed into
-// the other, one aligned 4-word block per locking step (mt_work), from the
-// current buffer and finished words of the next.  A draw uses 1/P(accept) <= 2
-// words on average, so a generation lasts >= ~312 draws and its successor is
-// ready after 156: the switch at index 624 is a bit flip, and no wave runs the
-// 624-word twist on the hot path (eagerly, a twisting wave took ~16k cycles,
-// 2x the others, and set the step's length whenever one occurred).  A
-// successor not ready in time (a host-written state restarts the progress at
-// 0) is finished wave-cooperatively (mt_finish).
+// the other, 64 words at a time: once per step every wave builds one 64-word
+// chunk of ONE of its envs' next generations (mt_chunk_*: the lowest lane
+// whose successor is incomplete), one word per lane, with coalesced 256-B
+// loads and stores -- 10 chunks per generation.  A draw uses 1/P(accept) <= 2
+// words on average, so a generation lasts >= ~312 draws (~1,500 steps at the
+// uniform-action lock rate); its wave has a chunk slot every step, and 64
+// envs x 10 chunks per ~1,500 steps use under half of them.  The switch at
+// index 624 is then a bit flip, and no wave runs the 624-word twist on the
+// hot path (eagerly, a twisting wave took ~16k cycles, 2x the others, and set
+// the step's length whenever one occurred).  (Round 1 built one 4-word block
+// per locking lane instead: its operand loads touched ~3 cache lines per
+// lock for ~36 bytes used.)  A successor not ready in time (a host-written or
+// synced state restarts the progress at 0) is finished wave-cooperatively
+// (mt_finish).
 //
 // Layout: cur[624..639] is next[0..15] for both parities -- B[0..15] for cur
 // = A; the pad, which the writers of A[0..15] also fill, for cur = B -- so a
@@ -262,7 +267,8 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
 //
 // State (stats row ST_STAT_MT_INDEX): idx | p << 10 | cur << 20
 //   idx: CPython's index into the current buffer (0..624)
-//   p  : words of the next generation done (multiple of 4, 0..624)
+//   p  : words of the next generation done (0..624; a multiple of 4 unless
+//        624: chunks start at any multiple of 4 a host state or mt_finish left)
 //   cur: 0 = A, 1 = B.
 // A host-written CPython index (p = cur = 0, state in A) is always valid;
 // st_mt_sync (k_mt_sync) brings every env back to that form.
@@ -323,32 +329,22 @@ __device__ __forceinline__ u32x4 mt_ld16(const MtRes &rs, bool on, uint32_t word
     return __builtin_amdgcn_raw_buffer_load_b128(rs.r, on ? rs.lane_off + 4u * word : kOff, 0, 0);
 }
 
-// Loaded for a locking lane before its lock path (consumed after it): the
-// draw window cur[idx..idx+7] and the operands of the next block.  Reads past
-// an env's state land in the next env's state or the allocation's back pad.
+// The draw window: MT words cur[idx + woff ..] of a locking lane, loaded
+// right after the lock decision and consumed by the draw.  Reads past an
+// env's state land in the next env's state or the allocation's back pad.
 struct MtPre {
-    uint32_t w[kMtWin], a[5], x[4];
+    uint32_t w[kMtWin];
 };
-// WIN = 16 for st_step; 8 in rollouts, where the second half measured slower
-// (register pressure in the k-step loop).
-// WIN: window words (0: none); OPS: the block operands.  (st_step: the draw
-// wave loads the window, the logic wave the operands.)
-template <int WIN, bool OPS = true>
+// WIN = 8 for st_step (after its 4-word draw-window cache: 12 words before a
+// dependent load, P(12 rejections) <= 2^-12); 16 in rollouts (no cache).
+template <int WIN>
 __device__ __forceinline__ void mt_pre_load(const MtRes &rs, uint32_t mtst, bool want, MtPre &q, int woff = 0) {
     int idx, pg, cur;
     mt_unpack(mtst, idx, pg, cur);
-    const uint32_t cb = cur ? kMtB : 0u, nb = cur ? 0u : kMtB;
-    const bool work = want && pg < kMtN;
-    u32x4 wv[WIN > 0 ? WIN / 4 : 1];
+    const uint32_t cb = cur ? kMtB : 0u;
+    u32x4 wv[WIN / 4];
 #pragma unroll
     for (int i = 0; i < WIN / 4; ++i) wv[i] = mt_ld16(rs, want, cb + idx + woff + 4 * i);
-    if constexpr (OPS) {
-        const u32x4 a = mt_ld16(rs, work, cb + pg);
-        const u32x4 x = mt_ld16(rs, work, pg <= 224 ? cb + pg + 397 : nb + pg - 227);
-        q.a[4] = __builtin_amdgcn_raw_buffer_load_b32(rs.r, work ? rs.lane_off + 4u * (cb + pg + 4) : kOff, 0, 0);
-        q.a[0] = a.x, q.a[1] = a.y, q.a[2] = a.z, q.a[3] = a.w;
-        q.x[0] = x.x, q.x[1] = x.y, q.x[2] = x.z, q.x[3] = x.w;
-    }
 #pragma unroll
     for (int i = 0; i < WIN / 4; ++i)
         q.w[4 * i] = wv[i].x, q.w[4 * i + 1] = wv[i].y, q.w[4 * i + 2] = wv[i].z, q.w[4 * i + 3] = wv[i].w;
@@ -364,29 +360,56 @@ __device__ __forceinline__ void mt_win_consume(const MtPre &q) {
         asm volatile("" ::"v"(q.w[8]), "v"(q.w[9]), "v"(q.w[10]), "v"(q.w[11]), "v"(q.w[12]),
                      "v"(q.w[13]), "v"(q.w[14]), "v"(q.w[15]));
 }
-__device__ __forceinline__ void mt_ops_consume(const MtPre &q) {
-    asm volatile("" ::"v"(q.a[0]), "v"(q.a[1]), "v"(q.a[2]), "v"(q.a[3]), "v"(q.a[4]), "v"(q.x[0]),
-                 "v"(q.x[1]), "v"(q.x[2]), "v"(q.x[3]));
-}
 
-// One block of the next generation, next[p..p+3] (lanes with `want` and
-// p < 624), as one 16-B store (+ the pad copy for next = A, p < 16).
-// AUX: kNT in st_step; plain in rollouts, whose later steps re-read the
-// blocks (X operands, the switch) from L2.
-template <int AUX>
-__device__ __forceinline__ void mt_work(const MtRes &rs, bool want, uint32_t &mtst, const MtPre &q) {
+// One 64-word chunk of one env's next generation per wave and step
+// (wave-uniform).  mt_chunk_issue picks the lowest lane whose successor is
+// incomplete and that has no preview straddling a generation switch (that
+// preview's words sit in the buffer the successor is built into, and
+// st_mt_sync may still give them back) and issues the operand loads:
+// lane i computes next[k], k = p + i:
+//   next[k] = X ^ mix(cur[k], cur[k + 1]),  X = cur[k + 397] (k < 227) | next[k - 227],
+// which covers new[623] too (cur[624] = next[0], see the layout).  Every
+// X = next[k - 227] lies >= 163 words below p: built by an earlier chunk.
+struct MtChunk {
+    uint32_t a0, a1, x;
+    uint32_t base;  // byte offset of the chosen env's buffer A in the wave's MT resource
+    int l;          // chosen lane (-1: none)
+    int pg, cur;    // its progress and current buffer
+};
+__device__ __forceinline__ void mt_chunk_issue(const MtRes &rs, uint32_t mtw, bool real, int lane, MtChunk &c) {
     int idx, pg, cur;
-    mt_unpack(mtst, idx, pg, cur);
-    const bool work = want && pg < kMtN;
-    uint4 v;
-    v.x = q.x[0] ^ mt_mix(q.a[0], q.a[1]);
-    v.y = q.x[1] ^ mt_mix(q.a[1], q.a[2]);
-    v.z = q.x[2] ^ mt_mix(q.a[2], q.a[3]);
-    v.w = q.x[3] ^ mt_mix(q.a[3], q.a[4]);
-    const uint32_t nb = cur ? 0u : kMtB;
-    buf_store16<AUX>(rs.r, work ? rs.lane_off + 4u * (nb + (uint32_t)pg) : kOff, v);
-    buf_store16<AUX>(rs.r, work && cur && pg < kMtWin ? rs.lane_off + 4u * (kMtPad + (uint32_t)pg) : kOff, v);
-    if (work) mtst = mt_keep(mtst, mt_pack(idx, pg + 4, cur));
+    mt_unpack(mtw, idx, pg, cur);
+    const int cc = (int)((mtw >> 25) & kPvCMax);
+    const bool cand = real && pg < kMtN && !(pv_ok(mtw) && idx <= cc);
+    // branch-free: a load issued on one path only would be merged with a
+    // zero at the join, and the merge waits for it on the spot (before B1)
+    const uint64_t m = __ballot(cand);
+    c.l = m ? (int)__builtin_ctzll(m) : -1;
+    const int l = m ? c.l : 0;
+    c.pg = __shfl(pg, l);
+    c.cur = __shfl(cur, l);
+    c.base = (uint32_t)l * (uint32_t)kMtPitch * 4u;
+    const int k = c.pg + lane;
+    const bool on = m != 0 && k < kMtN;
+    const uint32_t cb = c.cur ? kMtB : 0u, nb = c.cur ? 0u : kMtB;
+    const uint32_t xo = k < 227 ? cb + (uint32_t)k + 397u : nb + (uint32_t)k - 227u;
+    c.a0 = __builtin_amdgcn_raw_buffer_load_b32(rs.r, on ? c.base + 4u * (cb + (uint32_t)k) : kOff, 0, 0);
+    c.a1 = __builtin_amdgcn_raw_buffer_load_b32(rs.r, on ? c.base + 4u * (cb + (uint32_t)k + 1u) : kOff, 0, 0);
+    c.x = __builtin_amdgcn_raw_buffer_load_b32(rs.r, on ? c.base + 4u * xo : kOff, 0, 0);
+}
+// Compute and store the chunk (+ the pad copy of next[0..15] when next = A);
+// returns the chosen env's new progress.  AUX: kNT in st_step; plain in
+// rollouts, whose later steps read these words back (X operands, draws).
+template <int AUX>
+__device__ __forceinline__ int mt_chunk_store(const MtRes &rs, int lane, const MtChunk &c) {
+    const int k = c.pg + lane;
+    const bool on = c.l >= 0 && k < kMtN;
+    const uint32_t v = c.x ^ mt_mix(c.a0, c.a1);
+    const uint32_t nb = c.cur ? 0u : kMtB;
+    __builtin_amdgcn_raw_buffer_store_b32(v, rs.r, on ? c.base + 4u * (nb + (uint32_t)k) : kOff, 0, AUX);
+    __builtin_amdgcn_raw_buffer_store_b32(v, rs.r, on && c.cur && k < kMtWin ? c.base + 4u * (kMtPad + (uint32_t)k) : kOff,
+                                          0, AUX);
+    return c.pg + kWave < kMtN ? c.pg + kWave : kMtN;
 }
 
 // Finish the next generation of ONE env (words [pg, 624)), wave-cooperatively
@@ -530,7 +553,7 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
         const MtRes rs = mt_res(mt_wave, lane);
         do {
             // lanes at the end of their generation switch to the next one,
-            // finishing it first where mt_work has not
+            // finishing it first where the chunks have not
             const bool sw = pending && idx >= kMtN;
             uint64_t fin = __ballot(sw && pg < kMtN);
             while (fin) {
@@ -920,6 +943,14 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         }
     }
     ST_STAMP(2);
+    // the draw wave's next-generation chunk of this step: operands issued
+    // before B1, so they arrive while it waits for the lock decision
+    [[maybe_unused]] MtChunk chunk;
+    [[maybe_unused]] MtRes mrs;
+    if constexpr (DO_D) {
+        mrs = mt_res(p.mt + e0 * kMtPitch, lane);
+        mt_chunk_issue(mrs, mt0, real && !(kAblate & 2u), lane, chunk);
+    }
     if constexpr (TWO) {
         if constexpr (DO_L) {
             const uint64_t m = __ballot(locknow);
@@ -931,6 +962,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         wg_barrier();  // B1: the draw wave learns which lanes lock
         if constexpr (DO_D) ST_STAMP(10);
         if constexpr (DO_D && ST_DPRIO > 0) __builtin_amdgcn_s_setprio(ST_DPRIO);
+        if constexpr (DO_L && ST_LPRIO > 0) __builtin_amdgcn_s_setprio(ST_LPRIO);
         if constexpr (DO_D) {
             const uint32_t w = lane < 32 ? sm.lockm[t & 1][0] : sm.lockm[t & 1][1];
             locknow = (w >> (lane & 31)) & 1u;
@@ -940,33 +972,24 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         }
     }
 
-    // ---------------- draw: MT window + block operands, issued now ----------------
+    // ---------------- draw: MT window, issued now ----------------
     // Every locking lane draws (its next preview, or -- without a valid
-    // preview -- its piece first) and builds one block of its next generation
-    // (mt_work); the words are consumed after the lock path in one wave, or
-    // right away by the draw wave.
+    // preview -- its piece first); the window is consumed after the lock path
+    // in one wave, or right away by the draw wave.
     uint32_t mtst = mt0;  // packed (mt_pack + preview bits)
     const bool want_pre = locknow && !(kAblate & 2u);
-    constexpr int kWin = KSTEPS == 1 || TWO ? 16 : 8;
+    constexpr int kWin = STEP2 ? 8 : 16;
     MtPre pre;
-    [[maybe_unused]] MtRes mrs;
     // st_step: lanes whose draw-window cache is valid take their first 4 words
-    // from it (loaded with the state) and load the window 4 words further on
-    constexpr bool LWORK = STEP2 && ST_LWORK;
+    // from it (loaded after B0) and load the window 4 words further on
     [[maybe_unused]] const bool cv = STEP2 && cache_ok(mt0);
     [[maybe_unused]] const int woff = cv ? 4 : 0;
     if constexpr (DO_D) {
         // the cache words to the lane's LDS row before the window loads are
         // issued: their wait is here, not after the draw's branchy first-draw
         // path, where it would become a vmcnt(0) on the window
-        if constexpr (STEP2) *reinterpret_cast<uint4 *>(&sm.cw[lane * 20]) = c4v;
-        mrs = mt_res(p.mt + e0 * kMtPitch, lane);
-        if constexpr (LWORK) mt_pre_load<kWin, false>(mrs, mtst, want_pre, pre, woff);  // window only
-        else mt_pre_load<kWin>(mrs, mtst, want_pre, pre, woff);
-    }
-    if constexpr (LWORK && DO_L) {  // the logic wave builds the next-generation block
-        mrs = mt_res(p.mt + e0 * kMtPitch, lane);
-        mt_pre_load<0>(mrs, mtst, want_pre, pre);
+        if constexpr (STEP2) *reinterpret_cast<uint4 *>(&sm.cw[lane * 12]) = c4v;
+        mt_pre_load<kWin>(mrs, mtst, want_pre, pre, woff);
     }
 
     // ---------------- logic: lock path (tetris_env.py:263-299) ----------------
@@ -1154,16 +1177,6 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         } else {
             if (!spawn) paint<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
         }
-        if constexpr (LWORK) {
-            // next[pg..pg+3] (the draw wave counts it done in the MT word it
-            // commits; its own draws treat the block as pending: a finish it
-            // may run rewrites the same values)
-            if (!(kAblate & 2u)) {
-                mt_ops_consume(pre);
-                uint32_t mtw = mt0;
-                mt_work<kNT>(mrs, want_pre, mtw, pre);
-            }
-        }
     }
 
     ST_STAMP(8);  // (stamp 8: between the early stores and the draw)
@@ -1186,11 +1199,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         [[maybe_unused]] bool cvn = false;
         [[maybe_unused]] uint4 n4 = make_uint4(0u, 0u, 0u, 0u);
         if (!(kAblate & 2u)) {
-            if constexpr (!STEP2) {
-                mt_win_consume<kWin>(pre);
-                mt_ops_consume(pre);
-                mt_work<KSTEPS == 1 ? kNT : 0>(mrs, want_pre, mtst, pre);  // before the draws: a switch resets the progress
-            }
+            if constexpr (!STEP2) mt_win_consume<kWin>(pre);
             const bool need1 = dr_spec && !pv_ok(mt0);
             if (__ballot(need1)) {  // rare: after st_seed / st_mt_sync / a host-written state
                 const int pk = draw_shape<kWin, false>(need1, cnt, mtst, p.mt + e0 * kMtPitch, sm.S, lane, pre, false);
@@ -1212,35 +1221,29 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
                 // [cache | window] (positions i0.. of the draw's start) through
                 // a per-lane LDS row; valid only if the fast passes settled the
                 // draw and the 4 words lie inside the window and below lim
-                uint32_t *row = &sm.cw[lane * 20];  // row[0..3] = the cache (prologue)
+                uint32_t *row = &sm.cw[lane * 12];  // row[0..3] = the cache (stored before the draw)
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
+                for (int q = 0; q < kWin / 4; ++q)
                     *reinterpret_cast<uint4 *>(row + woff + 4 * q) =
                         make_uint4(pre.w[4 * q], pre.w[4 * q + 1], pre.w[4 * q + 2], pre.w[4 * q + 3]);
                 int i0, pg0, c0;
                 mt_unpack(m0, i0, pg0, c0);
                 const int lim0 = pg0 == kMtN ? kMtN + kWin : kMtN;
                 const int off = fpos - i0;
-                cvn = fpos >= 0 && off + 3 <= woff + 15 && fpos + 3 < lim0;
+                cvn = fpos >= 0 && off + 3 <= woff + kWin - 1 && fpos + 3 < lim0;
                 const int o = cvn ? off : 0;
                 n4 = make_uint4(row[o], row[o + 1], row[o + 2], row[o + 3]);
-                if constexpr (!LWORK) {  // the block, after the draw (its operands arrived under it)
-                    mt_ops_consume(pre);
-                    uint32_t mtw = mt0;
-                    mt_work<kNT>(mrs, want_pre, mtw, pre);
-                }
-                // this step's block counts unless a draw switched generations
-                // (which restarts the progress at 0)
-                int i1, pg1, c1, ia, pga, ca;
-                mt_unpack(mtst, i1, pg1, c1);
-                mt_unpack(mt0, ia, pga, ca);
-                if (want_pre && c1 == ca && pga < kMtN) mtst = mt_keep(mtst, mt_pack(i1, pga + 4, c1));
             }
             mt_new = pv_pack(mtst, npv, mt_consumed(m0, mtst), cvn);
         } else if constexpr (TWO) {
             sm.pick1[lane] = (uint32_t)sid;
             if (lane == 0) lds_flag_set(&sm.f2, (uint32_t)t + 1u);
         }
+        // this step's next-generation chunk (its operands arrived long ago);
+        // its env's progress advances unless that env's own draw switched
+        // generations (finishing the successor itself: same words)
+        const int chunk_pg = mt_chunk_store<KSTEPS == 1 ? kNT : 0>(mrs, lane, chunk);
+        const bool chunk_me = lane == chunk.l;
         ST_STAMP(4);
         if constexpr (STAMP) {  // 1: a draw started a generation, 2: a draw ran past its 8 words
             const int i0 = (int)(mt_before & 0x3FFu), i1 = (int)(mt_new & 0x3FFu);
@@ -1261,18 +1264,27 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
             const auto rc = buf_rsrc(p.mtc, (uint32_t)sd * 16u);
             buf_store16<kNT>(rc, dr && cvn ? (uint32_t)e * 16u : kOff, n4);
         }
+        // (a lane that locks but does not draw -- a death without auto-reset
+        // -- keeps its old MT word: its speculative draw is dropped)
+        uint32_t mt_out = dr ? mt_new : mt0;
+        if (chunk_me && (mt_out & (1u << 20)) == (mt0 & (1u << 20))) {
+            int i2, pg2, c2;
+            mt_unpack(mt_out, i2, pg2, c2);
+            mt_out = mt_keep(mt_out, mt_pack(i2, chunk_pg, c2));
+        }
+        if (dr || chunk_me) {
+            ss(ST_STAT_MT_INDEX) = mt_out;
+            sdd = 1u << ST_STAT_MT_INDEX;
+        }
         if (dr) {
-            // (a lane that locks but does not draw keeps its old MT word: the
-            // next-generation words mt_work stored are recomputed identically)
-            ss(ST_STAT_MT_INDEX) = mt_new;
             atomicAdd(&ss(ST_STAT_COUNT0 + sid), 1u);  // shape_counts[name] += 1, :199 (ds_add, no return)
-            sdd = (1u << ST_STAT_MT_INDEX) | (1u << (ST_STAT_COUNT0 + sid));
+            sdd |= 1u << (ST_STAT_COUNT0 + sid);
         }
         if constexpr (KSTEPS == 1) {
             if constexpr (TWO) sm.SDD[lane] = sdd;
             else sm.SD[lane] = sdd;  // the logic part ORs its rows in below
         } else if constexpr (TWO) {
-            sm.mtw[t & 1][lane] = dr ? mt_new : mt0;  // the logic wave's next step reads it after B1
+            sm.mtw[t & 1][lane] = mt_out;  // the logic wave's next step reads it after B1
         }
         ST_STAMP(11);
     }
