@@ -3,17 +3,21 @@
 
 Metric (BASELINE.json): env-steps/sec at 65,536 parallel 10x20 boards per GPU,
 1 -> 8 GPU weak scaling.  One "step" = one batched TetrisEngine.step
-(tetris_env.py:243-304) over every env of the job, fed by synthetic uniform
-actions a[t, e] = splitmix64(seed ^ ((t << 32) ^ e)) % 7 that are generated
-into HBM before the timed region.  Envs auto-reset inside the
-step kernel when they die (reference driver `if done: env.reset()`).
+(tetris_env.py:243-304) over every env of the job (one st_step launch per
+GPU), fed by synthetic uniform actions a[t, e] = splitmix64(seed ^ ((t << 32)
+^ e)) % 7 that are generated into HBM before the timed region.
+Envs auto-reset inside the step kernel when they die (the reference driver's
+`if done: env.reset()`).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c4] [--obs packed|f32] [--clear-heavy]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c4] [--obs packed|f32]
 
-N > 1 is launched by torch.distributed.run (one process per GPU, RCCL); each
-rank owns a contiguous block of global env indices and no collective runs in
-the timed steps ("scaling": "weak").  --gather additionally times one RCCL
-gather of every shard's packed obs/reward/done to rank 0 per step.
+--gpus N > 1: one process per GPU.  Run directly, bench.py starts the N rank
+processes itself (before anything touches a GPU) with the rendezvous on
+127.0.0.1; under torch.distributed.run it is one of the ranks.  Each rank owns
+a contiguous block of global env indices (seeds and actions keyed by the
+global index, so the work is identical at any N) and no collective runs in
+the timed steps ("scaling": "weak").  The RCCL gather of every shard's packed
+obs/reward/done to rank 0 (BASELINE config C5) is timed as `gather_variant`.
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -21,8 +25,11 @@ from __future__ import annotations
 import argparse
 import ctypes
 import glob
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,31 +37,41 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gym-simpletetris_amd"))
 sys.path.insert(0, ROOT)
 
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
+import torch  # noqa: E402  (importing torch does not initialise the GPU)
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 try:
     METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 except Exception:  # noqa: BLE001
-    METRIC = "env-steps/sec at 65 536 parallel 10\u00d720 boards; 1\u21928 GPU scaling"
+    METRIC = "env-steps/sec at 65 536 parallel 10×20 boards; 1→8 GPU scaling"
 
 CONFIGS = {
     # BASELINE.json configs[2] / [3]
     "c3": dict(),
     "c4": dict(advanced_clears=True, penalise_holes_increase=True, penalise_height_increase=True),
 }
+KERNEL_SOURCES = ("gym-simpletetris_amd/csrc/st_kernels.hip", "gym-simpletetris_amd/csrc/st_internal.h",
+                  "include/simpletetris.h")
+DEBUG = os.environ.get("ST_BENCH_DEBUG") == "1"
+REF_PY_STEPS_PER_S = 32752  # reference TetrisEnv.step(), 1 core of the build container
+
+
+# ----------------------------------------------------------------------------- bytes
+def s8d_bytes(p_lock: float, f32: bool) -> float:
+    """SURVEY §8(d)'s fixed formula, bytes per env-step: 182 + 184 p_lock
+    (packed obs) or 902 + 184 p_lock (float32 obs)."""
+    return (902.0 if f32 else 182.0) + 184.0 * p_lock
 
 
 def algorithmic_bytes(width: int, height: int, p_lock: float, f32: bool) -> float:
-    """Algorithmic HBM bytes per env-step of the step kernel.
-    Always: read action 1 + piece 4 + time 4 + board 4W; write piece 4 +
-    time 4 + reward 4 + done 1 + packed obs 4W (+ float32 obs 4WH).
-    Per lock: counters (score, lines, holes, piece_height, deaths, 7 counts,
-    MT index) read + written 2*13*4, board write 4W, MT words read 8, and the
-    amortised next MT generation (2 x 2,496 B read + 2,496 B written per
-    ~476 draws) 15.7."""
+    """Bytes per env-step the engine's column-packed layout needs:
+    102 + 167.7 p_lock at 10x20.  Always: read action 1 + piece 4 + time 4 +
+    board 4W; write piece 4 + time 4 + reward 4 + done 1 + packed obs 4W
+    (+ float32 obs 4WH).  Per lock: counters (score, lines, holes,
+    piece_height, deaths, 7 counts, MT index) read + written 2*13*4, board
+    write 4W, MT words read 8, and the amortised next MT generation
+    (2 x 2,496 B read + 2,496 B written per ~476 draws) 15.7."""
     always = (1 + 4 + 4 + 4 * width) + (4 + 4 + 4 + 1 + 4 * width)
     if f32:
         always += 4 * width * height
@@ -63,83 +80,147 @@ def algorithmic_bytes(width: int, height: int, p_lock: float, f32: bool) -> floa
 
 
 def rollout_bytes(width: int, height: int, p_lock: float, f32: bool, k: int) -> float:
-    """Algorithmic HBM bytes per env-step of the K-step rollout kernel: per
-    step read action 1, write packed obs 4W + reward 4 + done 1 (+ float32
-    obs 4WH); per lock MT words 8 + amortised next generation 15.7; per launch the state
-    (board 4W + 14 counters + piece) read and written once, / K."""
+    """Bytes per env-step of the K-step rollout kernel (I/O per
+    step + state r/w per K steps): per step read action 1, write packed obs 4W
+    + reward 4 + done 1 (+ float32 obs 4WH); per lock MT words 8 + amortised
+    next generation 15.7; per launch the state (board 4W + 14 counters +
+    piece) read and written once, / K."""
     step = 1 + 4 * width + 4 + 1 + (4 * width * height if f32 else 0)
     state = 2 * (4 * width + 15 * 4)
     return step + 23.7 * p_lock + state / k
 
 
-def cpu_baseline(seconds: float, cfg_kw: dict):
-    """Oracle (C restatement of the reference step, 1 core) on a bounded sample
-    of the same workload: 4,096 envs, same seeds/actions, auto-reset."""
-    from oracle import oracle as O
-    n = 4096
-    ob = O.OracleBatch(n, [1000 + e for e in range(n)], width=10, height=20, **cfg_kw)
-    ob.reset()
-    chunk = 64
-    t_steps = 0
-    t0 = time.perf_counter()
-    while True:
-        acts = O.splitmix64_actions(0x5EED, t_steps, chunk, n)
-        ob.rollout(acts, want_obs=True, want_stats=False)
-        t_steps += chunk
-        if time.perf_counter() - t0 >= seconds:
-            break
-    dt = time.perf_counter() - t0
-    return dict(value=n * t_steps / dt, unit="env-steps/s", cores=1, kind="port",
-                sample=f"C oracle (oracle/tetris_oracle.c), {n} envs x {t_steps} steps, "
-                       f"{dt:.1f} s on 1 host core, packed obs, auto-reset")
+# ----------------------------------------------------------------------------- PMC
+def kernel_source_sha() -> str:
+    """sha256 over the kernel sources: ties a PMC summary to the code it measured."""
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
-def load_pmc(kernel_prefix: str):
-    """Per-launch HBM traffic from the newest committed PMC summary, if any
-    (profiles/*_pmc.json written by tools/pmc_summary.py)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
-    for f in reversed(files):
+def load_pmc(kname: str, sha: str):
+    """Per-launch HBM bytes (FETCH+WRITE, gfx950-corrected by
+    tools/pmc_summary.py) of `kname` from a committed profiles/*_pmc.json whose
+    kernel-source hash equals the running sources'; (None, reason) if none."""
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), reverse=True):
         try:
             d = json.load(open(f))
         except Exception:  # noqa: BLE001
             continue
-        for k, v in d.get("kernels", {}).items():
-            if kernel_prefix in k:
-                return v.get("hbm_bytes_per_launch"), os.path.basename(f)
-    return None, None
+        if d.get("kernel_source_sha") != sha:
+            continue
+        v = d.get("kernels", {}).get(kname)
+        if v is not None:
+            return v.get("hbm_bytes_per_launch"), os.path.basename(f)
+    return None, f"no PMC pass of these kernel sources (sha {sha}) under profiles/"
 
 
+# ----------------------------------------------------------------------------- CPU baseline
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(seconds: float, config: str):
+    """The C oracle (a restatement of the reference step; the Python reference
+    cannot travel to the GPU box) on a bounded sample of the same workload:
+    4,096 envs per process, same seeds/actions, auto-reset.  One process on one
+    core, then one process per available core (capped at the box's 16-core
+    share) at once; `value` is the all-cores aggregate."""
+    cmd = [sys.executable, "-m", "oracle.cpu_bench", "--envs", "4096", "--seconds", str(seconds),
+           "--config", config]
+
+    def launch(p):
+        return subprocess.Popen(cmd + ["--offset", str(p * 4096)], cwd=ROOT, stdout=subprocess.PIPE,
+                                env=dict(os.environ, OMP_NUM_THREADS="1"))
+
+    def result(pr):
+        out, _ = pr.communicate()
+        if pr.returncode != 0:
+            raise RuntimeError(f"oracle.cpu_bench failed with {pr.returncode}")
+        return json.loads(out.decode().strip().splitlines()[-1])
+    one = result(launch(0))
+    single = one["env_steps"] / one["seconds"]
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    P = max(1, min(16, avail))
+    rs = [result(pr) for pr in [launch(p) for p in range(P)]]
+    agg = sum(r["env_steps"] / r["seconds"] for r in rs)
+    return dict(value=agg, unit="env-steps/s", cores=P, kind="port",
+                single_core=single, nproc=os.cpu_count(), cores_available=avail, cpu_model=cpu_model(),
+                sample=f"C oracle (oracle/tetris_oracle.c) on {P} processes x 4096 envs, "
+                       f"{rs[0]['steps']} steps each in ~{seconds:.0f} s (aggregate of per-process "
+                       f"rates); 1 process alone: {single:.4g} env-steps/s ({one['steps']} steps)",
+                reference_python_1core_build_container=REF_PY_STEPS_PER_S)
+
+
+# ----------------------------------------------------------------------------- launcher
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` run directly: start N rank processes (this parent
+    never touches a GPU), rendezvous on 127.0.0.1, return the worst exit code."""
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0:
+                rc = rc or r
+                for q in live:  # a failed rank would leave the others in a barrier
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+# ----------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=4000,
-                    help="timed steps (default spans >= 2 MT generations of a typical env, ~1,650 steps each)")
+                    help="timed steps (the default spans a next-MT-generation switch of most envs)")
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--n-envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c3")
     ap.add_argument("--obs", choices=("packed", "f32"), default="packed")
-    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a hipGraph")
-    ap.add_argument("--gather", action="store_true", help="also time a per-step RCCL gather")
+    ap.add_argument("--launch", choices=("graph", "eager"), default="graph",
+                    help="timed steps as one hipGraph of K st_step launches, or K eager launches")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--rollout-chunk", type=int, default=100, help="steps per st_rollout launch")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="timed region only (profiling)")
-    ap.add_argument("--clear-heavy", action="store_true",
-                    help="also time st_step on a greedy-player (line-clearing) action stream; off by "
-                         "default so that the headline kernel's rocprofv3 average covers only the "
-                         "headline workload")
+    ap.add_argument("--no-extras", action="store_true", help="headline only (profiling passes)")
+    ap.add_argument("--no-clear-heavy", action="store_true")
+    ap.add_argument("--gather-steps", type=int, default=200)
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # ST_BENCH_SHARED_GPU=1 (tests only): every rank on cuda:0, to exercise the
     # N>1 logic on a one-GPU box with --backend gloo
-    dev_idx = 0 if os.environ.get("ST_BENCH_SHARED_GPU") == "1" else local_rank
+    shared = os.environ.get("ST_BENCH_SHARED_GPU") == "1"
+    dev_idx = 0 if shared else local_rank
     torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx)
     if world > 1:
@@ -149,178 +230,207 @@ def main():
         else:
             dist.init_process_group(args.backend)
 
-    from gym_simpletetris_amd.distributed import ShardedTetris
+    from gym_simpletetris_amd import _lib as C
+    from gym_simpletetris_amd.distributed import ShardedTetris, output_buffer, buffer_views
 
-    n_local = args.n_envs
-    n_global = n_local * world
-    cfg_kw = CONFIGS[args.config]
     W, H = 10, 20
     K, WU = args.steps, args.warmup
     aseed = 0x5EED
-    sh = ShardedTetris(n_global, seed=1000, rank=rank, world=world, device=dev,
-                       autoreset="same_step", width=W, height=H, **cfg_kw)
-    eng = sh.engine
-    f32 = args.obs == "f32"
-    obs_f32 = torch.zeros((n_local, W, H), dtype=torch.float32, device=dev) if f32 else None
-    L = eng._L
-    from gym_simpletetris_amd import _lib as C
-
-    # inputs resident in HBM before timing
-    actions = torch.empty((WU + K, n_local), dtype=torch.uint8, device=dev)
-    for t in range(WU + K):
-        eng.gen_actions(t, aseed, global_offset=sh.offset, out=actions[t])
-    eng.reset()
-    obs_v, rew_v, done_v = buffer = (sh._obs, sh._rew, sh._done)
-    ctx = eng._ctx
-    p_obs, p_rew, p_done = (ctypes.c_void_p(x.data_ptr()) for x in buffer)
-    p_f32 = ctypes.c_void_p(obs_f32.data_ptr()) if f32 else None
-    act_ptrs = [ctypes.c_void_p(actions[t].data_ptr()) for t in range(WU + K)]
-
-    def step(t, stream):
-        if f32:
-            C.check(L.st_step_f32(ctx, act_ptrs[t], p_obs, p_f32, p_rew, p_done, stream))
-        else:
-            C.check(L.st_step(ctx, act_ptrs[t], p_obs, p_rew, p_done, stream))
-
     s = torch.cuda.Stream(dev)
     sp = ctypes.c_void_p(s.cuda_stream)
-    with torch.cuda.stream(s):
-        for t in range(WU):
-            step(t, sp)
-    torch.cuda.synchronize(dev)
+    sha = kernel_source_sha()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(s):  # an event's first record is slow (~100 us): not inside a timed region
+        ev0.record(s)
+        ev1.record(s)
 
-    def spawned():
-        st = eng.state_tensors(("stats",), sync=False)["stats"][6:13, :n_local]
+    def sync_all():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        if args.backend == "nccl":
+            t = torch.tensor([x], dtype=torch.float64, device=dev)
+        else:
+            t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def spawned(eng) -> int:
+        st = eng.state_tensors(("stats",), sync=False)["stats"][C.STAT["count0"]:C.STAT["count0"] + 7, :eng.n]
         return int(st.to(torch.int64).sum().item())
 
-    def timed(run, nsteps):
-        """Run `run()` (enqueues exactly nsteps steps on s) inside the timed
-        region: barrier + synchronize on both sides, max over ranks."""
-        c0 = spawned()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        with torch.cuda.stream(s):
-            ev0.record(s)
-            run()
+    def timed(eng, run, nsteps):
+        """Time `run()` (enqueues exactly nsteps steps of `eng` on s): barrier +
+        synchronize on both sides, max over ranks; events on s give the GPU
+        span.  p_lock from the spawn counters (every lock spawns one piece)."""
+        c0 = spawned(eng)
+        with torch.cuda.stream(s):  # s is current for the whole region (graph replay launches on it)
+            ev0.record(s)  # first host calls after a stream switch are slow: not inside the region
             ev1.record(s)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-        if world > 1:
-            tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            elapsed = float(tt.item())
-        # every lock spawns exactly one piece (the new piece, or the auto-reset's)
-        p_lock = (spawned() - c0) / float(n_local * nsteps)
+            sync_all()
+            t0 = time.perf_counter()
+            ev0.record(s)
+            t1 = time.perf_counter()
+            run()
+            t2 = time.perf_counter()
+            ev1.record(s)
+            t3 = time.perf_counter()
+            sync_all()
+            t4 = time.perf_counter()
+        elapsed = max_over_ranks(t4 - t0)
+        if DEBUG:
+            print("timed: rec0 %.1f run %.1f rec1 %.1f sync %.1f us" % ((t1 - t0) * 1e6, (t2 - t1) * 1e6,
+                  (t3 - t2) * 1e6, (t4 - t3) * 1e6), file=sys.stderr)
+        p_lock = (spawned(eng) - c0) / float(eng.n * nsteps)
         return elapsed, ev0.elapsed_time(ev1), p_lock
 
-    class _Eager:  # --no-graph (PMC passes): the same launches, eagerly
-        def __init__(self, use_f32):
-            self.f = use_f32
+    def make_actions(n, offset, gen):
+        a = torch.empty((WU + K, n), dtype=torch.uint8, device=dev)
+        for t in range(WU + K):
+            gen(t, aseed, global_offset=offset, out=a[t])
+        return a
 
-        def replay(self):
-            for t in range(WU, WU + K):
-                if self.f:
-                    C.check(L.st_step_f32(ctx, act_ptrs[t], p_obs, p_f32, p_rew, p_done, sp))
-                else:
-                    C.check(L.st_step(ctx, act_ptrs[t], p_obs, p_rew, p_done, sp))
-
-    def step_graph(use_f32):
-        if args.no_graph:
-            return _Eager(use_f32)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
-            for t in range(WU, WU + K):
-                if use_f32:
-                    C.check(L.st_step_f32(ctx, act_ptrs[t], p_obs, p_f32, p_rew, p_done, sp))
-                else:
-                    C.check(L.st_step(ctx, act_ptrs[t], p_obs, p_rew, p_done, sp))
-        torch.cuda.synchronize(dev)
-        return g
-
-    def roofline(kern_ms, bpe, launch_steps, kname):
-        achieved = bpe * n_local * launch_steps / (kern_ms * 1e-3) / 1e9
-        traffic, pmc_file = load_pmc(kname)
-        return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
-                "kernel_us": kern_ms * 1e3, "bytes_per_env_step": bpe,
-                "bytes_per_launch": bpe * n_local * launch_steps, "traffic_source": pmc_file}
-
-    # ---------------- headline: K single steps (st_step), graph-replayed ----------------
-    graph = step_graph(f32)
-
-    def run_main():
-        graph.replay()
-    elapsed, ev_ms, p_lock = timed(run_main, K)
-    value = n_global * K / elapsed
-    event_ms = ev_ms / K
-    sc0 = not cfg_kw  # no scoring flags: the SC0 specialization (st_kernels.hip launch_step)
-
-    def kname_of(kind, use_f32):  # rocprofv3's demangled name of the 10x20 kernel
+    def kname_of(kind, f32, sc0):  # rocprofv3's demangled name of the 10x20 kernel
         b = lambda v: "true" if v else "false"  # noqa: E731
         if kind == "step":
-            return f"k_step<10, 20, {b(use_f32)}, false, {b(sc0)}>"
-        return f"k_rollout<10, 20, {b(use_f32)}, {b(sc0)}>"
-    kname = kname_of("step", f32)
+            return f"k_step<10, 20, {b(f32)}, false, {b(sc0)}>"
+        return f"k_rollout<10, 20, {b(f32)}, {b(sc0)}>"
+
+    def roofline(kern_us, bpe, units_per_launch, kname, extra=None):
+        bpl = bpe * units_per_launch
+        achieved = bpl / (kern_us * 1e-6) / 1e9
+        traffic, src = load_pmc(kname, sha)
+        r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
+             "kernel_us": kern_us, "bytes_per_env_step": bpe, "bytes_per_launch": bpl,
+             "traffic_source": src, "kernel_source_sha": sha}
+        if extra:
+            r.update(extra)
+        return r
+
+    class Workload:
+        """One engine shard + its K+W action rows + reused output buffers."""
+
+        def __init__(self, n_local, cfg_kw, f32):
+            n_global = n_local * world
+            self.sh = ShardedTetris(n_global, seed=1000, rank=rank, world=world, device=dev,
+                                    autoreset="same_step", width=W, height=H, **cfg_kw)
+            self.eng = self.sh.engine
+            self.n_local, self.n_global = n_local, n_global
+            self.sc0 = not cfg_kw  # no scoring flags: the SC0 kernel specialization
+            self.f32 = f32
+            self.actions = make_actions(n_local, self.sh.offset, self.eng.gen_actions)
+            self.eng.reset()
+            torch.cuda.synchronize(dev)  # reset + actions (current stream) before s uses them
+            self.obs_f32 = torch.zeros((n_local, W, H), dtype=torch.float32, device=dev) if f32 else None
+            self.ptrs = [ctypes.c_void_p(x.data_ptr()) for x in (self.sh._obs, self.sh._rew, self.sh._done)]
+            self.pf = ctypes.c_void_p(self.obs_f32.data_ptr()) if f32 else None
+            self.aptr = [ctypes.c_void_p(self.actions[t].data_ptr()) for t in range(WU + K)]
+            L, ctx = self.eng._L, self.eng._ctx
+            po, pr, pd = self.ptrs
+            if f32:
+                self.launch = lambda t: C.check(L.st_step_f32(ctx, self.aptr[t], po, self.pf, pr, pd, sp))
+            else:
+                self.launch = lambda t: C.check(L.st_step(ctx, self.aptr[t], po, pr, pd, sp))
+
+        def warmup(self):
+            with torch.cuda.stream(s):
+                for t in range(WU):
+                    self.launch(t)
+            torch.cuda.synchronize(dev)
+
+        def runner(self):
+            if args.launch == "eager":
+                def run():
+                    for t in range(WU, WU + K):
+                        self.launch(t)
+                return run, None
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                for t in range(WU, WU + K):
+                    self.launch(t)
+            torch.cuda.synchronize(dev)
+            return g.replay, g
+
+        def measure(self):
+            self.warmup()
+            run, keep = self.runner()
+            el, ev_ms, p_lock = timed(self.eng, run, K)
+            del keep
+            kern_us = ev_ms * 1e3 / K
+            kname = kname_of("step", self.f32, self.sc0)
+            rl = roofline(kern_us, s8d_bytes(p_lock, self.f32), self.n_local, kname, {
+                "bytes_formula": "SURVEY 8(d): %d + 184 p_lock" % (902 if self.f32 else 182),
+                "frac_s8d": s8d_bytes(p_lock, self.f32) * self.n_local / (kern_us * 1e3) / HBM_PEAK_GBS,
+                "bytes_per_env_step_layout": algorithmic_bytes(W, H, p_lock, self.f32),
+                "frac_layout": algorithmic_bytes(W, H, p_lock, self.f32) * self.n_local
+                / (kern_us * 1e3) / HBM_PEAK_GBS,
+                "p_lock": p_lock})
+            if rl["traffic"] is not None:
+                rl["traffic_over_layout_bytes"] = rl["traffic"] / (rl["bytes_per_env_step_layout"] * self.n_local)
+            return {"value": self.n_global * K / el, "ms_per_step": el / K * 1e3,
+                    "event_ms_per_step": ev_ms / K, "p_lock": p_lock, "roofline": rl}
+
+        def close(self):
+            self.eng.close()
+
+    cfg_kw = CONFIGS[args.config]
+    f32 = args.obs == "f32"
+    head = Workload(args.n_envs, cfg_kw, f32)
+    hm = head.measure()
     out = {
         "metric": METRIC,
-        "value": value,
+        "value": hm["value"],
         "unit": "env-steps/s",
         "n_gpus": world,
         "steps": K,
         "warmup": WU,
-        "ms_per_step": elapsed / K * 1e3,
+        "ms_per_step": hm["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (uniform splitmix64 actions, seeds 1000 + global env index)",
         "config": {
-            "workload": f"{'C4' if args.config == 'c4' else 'C3'}: {n_local} parallel {W}x{H} boards "
-                        f"per GPU, one st_step per step, ram obs ({args.obs}), auto-reset, "
+            "workload": f"{args.config.upper()}: {args.n_envs} parallel {W}x{H} boards per GPU, one "
+                        f"st_step per step, ram obs ({args.obs}), auto-reset, "
                         + ("advanced_clears+penalise_holes_increase+penalise_height_increase"
                            if args.config == "c4" else "default rewards"),
-            "envs_per_gpu": n_local,
-            "envs_total": n_global,
+            "envs_per_gpu": args.n_envs,
+            "envs_total": head.n_global,
             "board": f"{W}x{H}",
             "obs": args.obs,
-            "launch": "eager" if args.no_graph else "hipGraph of K st_step launches",
+            "launch": ("hipGraph of K st_step launches" if args.launch == "graph"
+                       else "K eager st_step launches"),
             "parallelism": f"env-shard x{world}",
         },
-        "p_lock": p_lock,
-        "event_ms_per_step": event_ms,
-        # graph launches run back to back (rocprofv3: ~0 gap), so the event
-        # time of the timed region / K is the kernel's average duration
-        "roofline": roofline(event_ms, algorithmic_bytes(W, H, p_lock, f32), 1, kname),
+        "p_lock": hm["p_lock"],
+        "event_ms_per_step": hm["event_ms_per_step"],
+        "roofline": hm["roofline"],
     }
-    del graph
 
     if not args.no_extras:
         variants = {}
+        eng = head.eng
+        L, ctx = eng._L, eng._ctx
         if not f32:  # the same st_step with the reference's float32 obs fused in
-            if obs_f32 is None:  # keep the tensor alive while graphs/launches use it
-                obs_f32 = torch.zeros((n_local, W, H), dtype=torch.float32, device=dev)
-                p_f32 = ctypes.c_void_p(obs_f32.data_ptr())
-            g = step_graph(True)
-            el, ev, pl = timed(g.replay, K)
-            variants["step_f32"] = {
-                "value": n_global * K / el, "ms_per_step": el / K * 1e3, "p_lock": pl,
-                "roofline": roofline(ev / K, algorithmic_bytes(W, H, pl, True), 1,
-                                     kname_of("step", True))}
-            del g
-        # K-step rollout kernel (st_rollout): CH steps per launch
+            w = Workload(args.n_envs, cfg_kw, True)
+            variants["step_f32"] = w.measure()
+            w.close()
+        # K-step rollout kernel (st_rollout), continuing the headline's state
         CH = min(args.rollout_chunk, K)
         nch = K // CH
+        n_local = head.n_local
         ro = torch.empty((CH, W, n_local), dtype=torch.int32, device=dev)
         rr = torch.empty((CH, n_local), dtype=torch.int32, device=dev)
         rd = torch.empty((CH, n_local), dtype=torch.uint8, device=dev)
         for use_f32 in (False, True):
             rf = torch.empty((CH, n_local, W, H), dtype=torch.float32, device=dev) if use_f32 else None
-            aptr = [ctypes.c_void_p(actions[WU + c * CH].data_ptr()) for c in range(nch)]
+            aptr = [ctypes.c_void_p(head.actions[WU + c * CH].data_ptr()) for c in range(nch)]
             ptrs = [ctypes.c_void_p(x.data_ptr()) if x is not None else None for x in (ro, rf, rr, rd)]
 
             def run_ro():
@@ -328,83 +438,137 @@ def main():
                     C.check(L.st_rollout(ctx, CH, aptr[c], *ptrs, sp))
             with torch.cuda.stream(s):  # warm-up launch
                 C.check(L.st_rollout(ctx, CH, aptr[0], *ptrs, sp))
-            el, ev, pl = timed(run_ro, nch * CH)
-            key = "rollout_f32" if use_f32 else "rollout_packed"
-            variants[key] = {
-                "value": n_global * nch * CH / el, "ms_per_step": el / (nch * CH) * 1e3,
+            el, ev, pl = timed(eng, run_ro, nch * CH)
+            kern_us = ev * 1e3 / nch
+            variants["rollout_f32" if use_f32 else "rollout_packed"] = {
+                "value": head.n_global * nch * CH / el, "ms_per_step": el / (nch * CH) * 1e3,
                 "steps_per_launch": CH, "p_lock": pl,
-                "roofline": roofline(ev / nch, rollout_bytes(W, H, pl, use_f32, CH), CH,
-                                     kname_of("rollout", use_f32))}
+                "roofline": roofline(kern_us, rollout_bytes(W, H, pl, use_f32, CH), CH * n_local,
+                                     kname_of("rollout", use_f32, head.sc0),
+                                     {"bytes_formula": "rollout: I/O per step + state r/w per launch / K",
+                                      "p_lock": pl})}
             del rf
-
-        def clear_heavy(variants):
-            # Clear-heavy regime: uniform actions almost never clear
-            # a line, so the same st_step is also timed on an action stream that
-            # a greedy placement player (st_policy_greedy, 3% random) produced from
-            # the same start state: recorded untimed, then replayed from a
-            # snapshot of that start state through the same hipGraph path.
-            ce = ShardedTetris(n_global, seed=1000, rank=rank, world=world, device=dev,
-                               autoreset="same_step", width=W, height=H, **cfg_kw).engine
-            ce.reset()
-            snap = ce.save()
-            gact = torch.empty((WU + K, n_local), dtype=torch.uint8, device=dev)
-            cleared = torch.zeros((), dtype=torch.int64, device=dev)
-            with torch.cuda.stream(s):
-                for t in range(WU + K):
-                    ce.policy_greedy(t, seed=aseed, explore=30, out=gact[t])
-                    C.check(L.st_step(ce._ctx, ctypes.c_void_p(gact[t].data_ptr()), p_obs, p_rew, p_done, sp))
-                    if t >= WU:  # default rewards: +100 per cleared line
-                        cleared += rew_v.clamp(min=0).sum()
-            torch.cuda.synchronize(dev)
-            n_cleared = int(cleared.item())
-            ce.load(snap)
-            del snap
-            gptr = [ctypes.c_void_p(gact[t].data_ptr()) for t in range(WU + K)]
-            with torch.cuda.stream(s):
-                for t in range(WU):
-                    C.check(L.st_step(ce._ctx, gptr[t], p_obs, p_rew, p_done, sp))
-            torch.cuda.synchronize(dev)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=s):
-                for t in range(WU, WU + K):
-                    C.check(L.st_step(ce._ctx, gptr[t], p_obs, p_rew, p_done, sp))
-            torch.cuda.synchronize(dev)
-            el, ev, _ = timed(g.replay, K)
-            variants["step_clear_heavy"] = {
-                "value": n_global * K / el, "ms_per_step": el / K * 1e3,
-                "lines_per_env_step": (n_cleared / 100.0 / (n_local * K)) if args.config == "c3" else None,
-                "actions": "st_policy_greedy (greedy placement, 3% uniform), recorded then replayed",
-                "kernel_us": ev / K * 1e3}
-            del g, ce
-
-        if args.clear_heavy:
-            clear_heavy(variants)
+        # the other single-GPU BASELINE configs: C2 (4,096 boards), C4 / C3
+        other = "c3" if args.config == "c4" else "c4"
+        w = Workload(args.n_envs, CONFIGS[other], f32)
+        variants[other] = w.measure()
+        variants[other]["config"] = f"{other.upper()} at {args.n_envs} boards per GPU"
+        w.close()
+        w = Workload(4096, cfg_kw, f32)
+        variants["c2"] = w.measure()
+        variants["c2"]["config"] = f"C2: 4096 boards per GPU, {args.config.upper()} rewards"
+        w.close()
+        if not args.no_clear_heavy and not f32:
+            variants["step_clear_heavy"] = clear_heavy(head, cfg_kw, C, ShardedTetris, timed, roofline,
+                                                       kname_of, dev, s, sp, rank, world, W, H, K, WU,
+                                                       aseed, args.config)
         out["variants"] = variants
-        if args.gather and world > 1:
-            torch.cuda.synchronize(dev)
-            dist.barrier()
-            g0 = time.perf_counter()
-            G = min(K, 200)
-            for i in range(G):
-                with torch.cuda.stream(s):
-                    step(WU + i, sp)
-                s.synchronize()
-                sh.gather(cpu=args.backend != "nccl")
-            torch.cuda.synchronize(dev)
-            dist.barrier()
-            gdt = time.perf_counter() - g0
-            tt = torch.tensor([gdt], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            gdt = float(tt.item())
-            out["gather_variant"] = {"value": n_global * G / gdt, "ms_per_step": gdt / G * 1e3,
-                                     "steps": G, "bytes_per_rank_per_step": sh.buf.numel() * 4,
-                                     "note": "eager st_step + RCCL gather of packed obs/reward/done to rank 0"}
+        if world > 1:
+            out["gather_variant"] = gather_variant(head, args, C, output_buffer, buffer_views,
+                                                   dev, s, sp, rank, world, W, WU, max_over_ranks)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cfg_kw)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.config)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
+
+
+def clear_heavy(head, cfg_kw, C, ShardedTetris, timed, roofline, kname_of, dev, s, sp, rank, world,
+                W, H, K, WU, aseed, config):
+    """Clear-heavy regime: uniform actions almost never clear a
+    line, so the same st_step is also timed on an action stream that a greedy
+    placement player (st_policy_greedy, 3% random) produced from the same start
+    state: recorded untimed, then replayed from a snapshot of that start state
+    through the same launch path."""
+    n_global = head.n_global
+    ce = ShardedTetris(n_global, seed=1000, rank=rank, world=world, device=dev,
+                       autoreset="same_step", width=W, height=H, **cfg_kw).engine
+    L = ce._L
+    po, pr, pd = head.ptrs
+    rew = head.sh._rew
+    ce.reset()
+    torch.cuda.synchronize(dev)
+    snap = ce.save()
+    gact = torch.empty((WU + K, ce.n), dtype=torch.uint8, device=dev)
+    cleared = torch.zeros((), dtype=torch.int64, device=dev)
+    with torch.cuda.stream(s):
+        for t in range(WU + K):
+            ce.policy_greedy(t, seed=aseed, explore=30, out=gact[t])
+            C.check(L.st_step(ce._ctx, ctypes.c_void_p(gact[t].data_ptr()), po, pr, pd, sp))
+            if t >= WU and config == "c3":  # default rewards: +100 per cleared line
+                cleared += rew.clamp(min=0).sum()
+    torch.cuda.synchronize(dev)
+    n_cleared = int(cleared.item())
+    ce.load(snap)
+    gptr = [ctypes.c_void_p(gact[t].data_ptr()) for t in range(WU + K)]
+    with torch.cuda.stream(s):
+        for t in range(WU):
+            C.check(L.st_step(ce._ctx, gptr[t], po, pr, pd, sp))
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        for t in range(WU, WU + K):
+            C.check(L.st_step(ce._ctx, gptr[t], po, pr, pd, sp))
+    torch.cuda.synchronize(dev)
+    el, ev, pl = timed(ce, g.replay, K)
+    kern_us = ev * 1e3 / K
+    bpe = (182.0 + 184.0 * pl)
+    r = {"value": n_global * K / el, "ms_per_step": el / K * 1e3, "p_lock": pl,
+         "lines_per_env_step": (n_cleared / 100.0 / (ce.n * K)) if config == "c3" else None,
+         "actions": "st_policy_greedy (greedy placement, 3% uniform), recorded then replayed",
+         "roofline": roofline(kern_us, bpe, ce.n, kname_of("step", False, not cfg_kw),
+                              {"bytes_formula": "SURVEY 8(d): 182 + 184 p_lock", "p_lock": pl})}
+    del g
+    ce.close()
+    return r
+
+
+def gather_variant(head, args, C, output_buffer, buffer_views, dev, s, sp, rank, world, W, WU,
+                   max_over_ranks):
+    """BASELINE config C5's exchange: each step's packed obs/reward/done of
+    every shard gathered to rank 0 (torch.distributed.gather; RCCL over xGMI
+    with the nccl backend).  Double-buffered: the gather of step t runs on the
+    collective stream while step t+1 computes into the other buffer."""
+    G = min(args.gather_steps, args.steps)
+    eng = head.eng
+    L, ctx = eng._L, eng._ctx
+    n = head.n_local
+    nccl = args.backend == "nccl"
+    bufs = [output_buffer(W, n, dev) for _ in range(2)]
+    views = [[ctypes.c_void_p(v.data_ptr()) for v in buffer_views(b, W)] for b in bufs]
+    recv = [[torch.empty_like(b) for _ in range(world)] if rank == 0 else None for b in bufs]
+    if not nccl:  # gloo: host tensors, no overlap
+        recv = [[torch.empty_like(b, device="cpu") for _ in range(world)] if rank == 0 else None
+                for b in bufs]
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    works = [None, None]
+    for i in range(G):
+        k = i & 1
+        with torch.cuda.stream(s):
+            if works[k] is not None:
+                works[k].wait()  # s waits for the gather that still reads bufs[k]
+            C.check(L.st_step(ctx, head.aptr[WU + i], *views[k], sp))
+            if nccl:
+                works[k] = dist.gather(bufs[k], gather_list=recv[k], dst=0, async_op=True)
+            else:
+                s.synchronize()
+                dist.gather(bufs[k].cpu(), gather_list=recv[k], dst=0)
+    with torch.cuda.stream(s):
+        for w in works:
+            if w is not None:
+                w.wait()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    gdt = max_over_ranks(time.perf_counter() - t0)
+    return {"value": head.n_global * G / gdt, "ms_per_step": gdt / G * 1e3, "steps": G,
+            "bytes_per_rank_per_step": bufs[0].numel() * 4,
+            "backend": args.backend,
+            "note": "eager st_step + gather of packed obs/reward/done to rank 0 every step, "
+                    "double-buffered so step t+1 overlaps the gather of step t"}
 
 
 if __name__ == "__main__":
