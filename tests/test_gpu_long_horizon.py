@@ -1,0 +1,195 @@
+"""The timed bench workload itself, at full size and over the bench's horizon,
+bit-exact against the C oracle (VERDICT r1 "next" #1).
+
+bench.py times 65,536 envs (seeds 1000 + e), synthetic actions
+splitmix64(0x5EED ^ (t << 32 ^ e)) % 7, same-step auto-reset, W eager warm-up
+st_step launches and then K st_step launches captured in one hipGraph.  These
+tests run exactly that (W = 100, K = 4,000: a second MT generation switch for
+most envs, boards at full occupancy, every auto-reset path) with each step's
+outputs written to its own slot, and compare every step's reward, done and
+packed obs, then the final board / piece / counters / MT19937 state, with the
+oracle (TetrisEngine.step restated, tetris_env.py:243-304; CPython's random,
+:183-191), for BASELINE configs C3 and C4.  The same for st_rollout: 10
+launches of 100 steps.  The oracle runs on host threads over env slices
+(ctypes releases the GIL), so the check takes seconds.
+"""
+import ctypes
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+N, W, H = 65536, 10, 20
+WU, K = 100, 4000
+SEED_BASE, ASEED = 1000, 0x5EED
+CONFIGS = {
+    "c3": dict(),
+    "c4": dict(advanced_clears=True, penalise_holes_increase=True, penalise_height_increase=True),
+}
+
+
+def _threads():
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(16, n))
+
+
+class ParallelOracle:
+    """N oracle envs split into contiguous slices, one host thread each;
+    global env index e keeps seed SEED_BASE + e and the action stream of e."""
+
+    def __init__(self, n, kw, parts=None):
+        parts = parts or _threads()
+        bounds = np.linspace(0, n, parts + 1).astype(int)
+        self.sl = [(int(a), int(b)) for a, b in zip(bounds[:-1], bounds[1:]) if b > a]
+        self.obs = [O.OracleBatch(b - a, [SEED_BASE + a + e for e in range(b - a)], width=W, height=H, **kw)
+                    for a, b in self.sl]
+        for ob in self.obs:
+            ob.reset()
+        self.pool = ThreadPoolExecutor(len(self.sl))
+
+    def rollout(self, t0, T):
+        def one(i):
+            a, b = self.sl[i]
+            acts = O.splitmix64_actions(ASEED, t0, T, b - a, offset=a)
+            return self.obs[i].rollout(acts, want_obs=True, want_stats=False)
+        rs = list(self.pool.map(one, range(len(self.sl))))
+        return {k: np.concatenate([r[k] for r in rs], axis=1) for k in ("reward", "done", "obs")}
+
+    def final_state(self):
+        """Structured view of every env (Env struct fields) in global order."""
+        return np.concatenate([np.ctypeslib.as_array(ob.envs) for ob in self.obs])
+
+    def close(self):
+        self.pool.shutdown()
+
+
+def _pack_board(board_u8):
+    """oracle board [n][OR_MAX_W][OR_MAX_H] u8 -> packed columns [W][n] u32 (bit y of word x)."""
+    b = (board_u8[:, :W, :H] != 0).astype(np.uint64)
+    return (b << np.arange(H, dtype=np.uint64)).sum(axis=2).astype(np.uint32).T
+
+
+def _seeded_words(n):
+    """random.seed(SEED_BASE + e) words of every env (the oracle's seeding)."""
+    out = np.empty((n, 624), np.uint32)
+    for e in range(n):
+        out[e] = np.ctypeslib.as_array(O.MTRandom(SEED_BASE + e)._mt.mt)
+    return out
+
+
+def _twist_np(w):
+    """One MT19937 refill of every row (CPython genrand_uint32 at index 624)."""
+    w = w.astype(np.uint32).copy()
+    for k in range(624):
+        y = (w[:, k] & np.uint32(0x80000000)) | (w[:, (k + 1) % 624] & np.uint32(0x7FFFFFFF))
+        w[:, k] = w[:, (k + 397) % 624] ^ (y >> np.uint32(1)) ^ np.where(y & np.uint32(1), np.uint32(0x9908B0DF),
+                                                                       np.uint32(0))
+    return w
+
+
+def _check_final(eng, orc):
+    st = eng.get_state()  # st_mt_sync first: CPython's exact MT state
+    ref = orc.final_state()
+    stats = st["stats"]
+    for row, field in ((0, "time"), (1, "score"), (2, "lines_cleared"), (3, "holes"),
+                       (4, "piece_height"), (5, "n_deaths")):
+        assert np.array_equal(stats[row], ref[field]), field
+    assert np.array_equal(stats[6:13].T, ref["counts"]), "shape counts"
+    p = st["piece"]
+    for name, got in (("shape_id", p & 7), ("rot", (p >> 3) & 3), ("ax", (p >> 5) & 63),
+                      ("ay", (p >> 11) & 63), ("lock", p >> 17)):
+        assert np.array_equal(got.astype(np.int64), ref[name].astype(np.int64)), name
+    assert np.array_equal(st["board"], _pack_board(ref["board"])), "board"
+    assert np.array_equal(stats[13], ref["rng"]["index"]), "MT index"
+    assert np.array_equal(st["mt"], ref["rng"]["mt"].astype(np.uint32)), "MT words"
+
+
+def _compare(t0, got_r, got_d, got_o, ref):
+    assert np.array_equal(got_r, ref["reward"]), f"reward, steps {t0}.."
+    assert np.array_equal(got_d.astype(np.uint8), ref["done"]), f"done, steps {t0}.."
+    bad = np.argwhere((got_o.transpose(0, 2, 1) != ref["obs"]).any(axis=2))
+    assert bad.size == 0, f"obs mismatch at (step, env) {bad[:4] + [t0, 0]}"
+
+
+@pytest.mark.parametrize("config", sorted(CONFIGS))
+def test_bench_workload_st_step_graph(config):
+    import gym_simpletetris_amd as G
+    from gym_simpletetris_amd import _lib as C
+    dev = torch.device("cuda", 0)
+    kw = CONFIGS[config]
+    eng = G.TetrisBatch(N, autoreset="same_step", seeds=[SEED_BASE + e for e in range(N)],
+                        device=dev, width=W, height=H, **kw)
+    T = WU + K
+    acts = torch.empty((T, N), dtype=torch.uint8, device=dev)
+    for t in range(T):
+        eng.gen_actions(t, ASEED, out=acts[t])
+    eng.reset()
+    obs = torch.empty((T, W, N), dtype=torch.int32, device=dev)
+    rew = torch.empty((T, N), dtype=torch.int32, device=dev)
+    done = torch.empty((T, N), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+    L, ctx = eng._L, eng._ctx
+    s = torch.cuda.Stream(dev)
+    sp = ctypes.c_void_p(s.cuda_stream)
+
+    def launch(t):
+        C.check(L.st_step(ctx, ctypes.c_void_p(acts[t].data_ptr()), ctypes.c_void_p(obs[t].data_ptr()),
+                          ctypes.c_void_p(rew[t].data_ptr()), ctypes.c_void_p(done[t].data_ptr()), sp))
+    with torch.cuda.stream(s):
+        for t in range(WU):  # bench warm-up: eager launches
+            launch(t)
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):  # bench timed region: one graph of K launches
+        for t in range(WU, T):
+            launch(t)
+    with torch.cuda.stream(s):
+        g.replay()
+    torch.cuda.synchronize(dev)
+    del g
+    orc = ParallelOracle(N, kw)
+    try:
+        CH = 100
+        for t0 in range(0, T, CH):
+            ref = orc.rollout(t0, CH)
+            _compare(t0, rew[t0:t0 + CH].cpu().numpy(), done[t0:t0 + CH].cpu().numpy(),
+                     obs[t0:t0 + CH].cpu().numpy().view(np.uint32), ref)
+        _check_final(eng, orc)
+        # the regime the bench times: most envs went past their first generation
+        fin = orc.final_state()["rng"]["mt"].astype(np.uint32)
+        gen1 = _twist_np(_seeded_words(N))
+        assert (fin != gen1).any(axis=1).mean() > 0.5
+    finally:
+        orc.close()
+        eng.close()
+
+
+@pytest.mark.parametrize("config", sorted(CONFIGS))
+def test_bench_workload_st_rollout(config):
+    import gym_simpletetris_amd as G
+    dev = torch.device("cuda", 0)
+    kw = CONFIGS[config]
+    eng = G.TetrisBatch(N, autoreset="same_step", seeds=[SEED_BASE + e for e in range(N)],
+                        device=dev, width=W, height=H, **kw)
+    CH, NL = 100, 10
+    acts = torch.empty((CH * NL, N), dtype=torch.uint8, device=dev)
+    for t in range(CH * NL):
+        eng.gen_actions(t, ASEED, out=acts[t])
+    eng.reset()
+    orc = ParallelOracle(N, kw)
+    buf = {}
+    try:
+        for c in range(NL):
+            o, r, d = eng.rollout(acts[c * CH:(c + 1) * CH], obs="packed", out=buf)
+            ref = orc.rollout(c * CH, CH)
+            _compare(c * CH, r.cpu().numpy(), d.cpu().numpy(), o.cpu().numpy().view(np.uint32), ref)
+        _check_final(eng, orc)
+    finally:
+        orc.close()
+        eng.close()
