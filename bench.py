@@ -458,10 +458,11 @@ def main():
         variants["c2"] = w.measure()
         variants["c2"]["config"] = f"C2: 4096 boards per GPU, {args.config.upper()} rewards"
         w.close()
+        variants.update(image_variants(head, C, timed, roofline, dev, s, sp, W, WU, K))
         if not args.no_clear_heavy and not f32:
             variants["step_clear_heavy"] = clear_heavy(head, cfg_kw, C, ShardedTetris, timed, roofline,
                                                        kname_of, dev, s, sp, rank, world, W, H, K, WU,
-                                                       aseed, args.config)
+                                                       aseed, args.config, args.launch)
         out["variants"] = variants
         if world > 1:
             out["gather_variant"] = gather_variant(head, args, C, output_buffer, buffer_views,
@@ -475,8 +476,51 @@ def main():
         dist.destroy_process_group()
 
 
+def image_variants(head, C, timed, roofline, dev, s, sp, W, WU, K):
+    """obs_type='grayscale' / 'rgb' (tetris_env.py:76-122, :426-433): the
+    84x84 float32 image of every env per step (st_grayscale on st_step's
+    packed obs).  Timed two ways: the image kernel alone on one packed obs
+    (its roofline: reads 4W B + writes 84*84*ch*4 B per env), and whole steps
+    (st_step + st_grayscale per step)."""
+    eng = head.eng
+    L, ctx = eng._L, eng._ctx
+    n = head.n_local
+    KG = max(1, min(K, 200))
+    out = {}
+    po, pr, pd = head.ptrs
+    for name, ch in (("grayscale_f32", 1), ("rgb_f32", 3)):
+        img = torch.empty((n, 84, 84, ch), dtype=torch.float32, device=dev)
+        pi = ctypes.c_void_p(img.data_ptr())
+
+        def run_img():
+            for _ in range(KG):
+                C.check(L.st_grayscale(ctx, po, 84, ch, 0, pi, sp))
+        with torch.cuda.stream(s):
+            run_img()
+        el, ev, _ = timed(eng, run_img, KG)
+        kern_us = ev * 1e3 / KG
+        bpe = 4 * W + 84 * 84 * ch * 4
+        r = {"kernel_only": True, "launches": KG, "kernel_us": kern_us,
+             "roofline": roofline(kern_us, bpe, n, "k_grayscale<float>",
+                                  {"bytes_formula": f"read packed obs 4W + write 84*84*{ch}*4 per env"})}
+        # whole steps with this obs_type: st_step + the image per step
+        KS = max(1, min(K, 100))
+
+        def run_steps():
+            for t in range(WU, WU + KS):
+                C.check(L.st_step(ctx, head.aptr[t], po, pr, pd, sp))
+                C.check(L.st_grayscale(ctx, po, 84, ch, 0, pi, sp))
+        el, ev, pl = timed(eng, run_steps, KS)
+        r.update({"value": head.n_global * KS / el, "ms_per_step": el / KS * 1e3, "steps": KS,
+                  "note": "value: env-steps/s of st_step + st_grayscale (obs_type=%r), eager launches"
+                          % ("grayscale" if ch == 1 else "rgb")})
+        out[name] = r
+        del img
+    return out
+
+
 def clear_heavy(head, cfg_kw, C, ShardedTetris, timed, roofline, kname_of, dev, s, sp, rank, world,
-                W, H, K, WU, aseed, config):
+                W, H, K, WU, aseed, config, launch):
     """Clear-heavy regime: uniform actions almost never clear a
     line, so the same st_step is also timed on an action stream that a greedy
     placement player (st_policy_greedy, 3% random) produced from the same start
@@ -507,12 +551,16 @@ def clear_heavy(head, cfg_kw, C, ShardedTetris, timed, roofline, kname_of, dev, 
         for t in range(WU):
             C.check(L.st_step(ce._ctx, gptr[t], po, pr, pd, sp))
     torch.cuda.synchronize(dev)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=s):
+    def run_eager():
         for t in range(WU, WU + K):
             C.check(L.st_step(ce._ctx, gptr[t], po, pr, pd, sp))
-    torch.cuda.synchronize(dev)
-    el, ev, pl = timed(ce, g.replay, K)
+    g = None
+    if launch == "graph":
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            run_eager()
+        torch.cuda.synchronize(dev)
+    el, ev, pl = timed(ce, g.replay if g is not None else run_eager, K)
     kern_us = ev * 1e3 / K
     bpe = (182.0 + 184.0 * pl)
     r = {"value": n_global * K / el, "ms_per_step": el / K * 1e3, "p_lock": pl,

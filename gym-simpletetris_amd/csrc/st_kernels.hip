@@ -1702,53 +1702,137 @@ __global__ __launch_bounds__(kWave) void k_render(KParams p) {
 }
 
 // ---------------------------------------------------------------- misc
-// packed obs [W][n] -> float32 [n][W][H] (TetrisEnv.step float32 cast, :400).
-__global__ void k_obs_f32(const uint32_t *__restrict__ obs, float *__restrict__ out, int64_t n,
-                          int W, int H) {
-    const int64_t total = n * W * H;
-    for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < total;
-         f += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t e = f / (W * H);
-        const int rem = (int)(f - e * W * H);
-        const int x = rem / H;
-        const int y = rem - x * H;
-        out[f] = (float)((obs[x * n + e] >> y) & 1u);
+// Image writers: the output of a block of envs is one contiguous region, so
+// lanes walk it in 16-B chunks (lane-consecutive vector stores, one 1-KB
+// burst per wave instruction, non-temporal: the images stream past L2), and
+// each chunk's elements are decoded from the block's packed obs words staged
+// in LDS.  Reads are 4 B per env per board column, coalesced over the
+// block's envs.
+constexpr int kImgEnvs = 16;  // envs per block: 64-B obs row segments
+constexpr int kMaxImg = 4096;  // largest image side (st_grayscale checks)
+
+template <typename T>
+__device__ __forceinline__ void store16_nt(T *dst, const T (&v)[16 / sizeof(T)]) {
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    u4 w;
+    __builtin_memcpy(&w, v, 16);
+    __builtin_nontemporal_store(w, reinterpret_cast<u4 *>(dst));
+}
+
+// packed obs [W][n] -> float32 [n][W][H] (TetrisEnv.step float32 cast, :400):
+// 64 envs per block, element (e, x, y) = bit y of word (x, e).
+__global__ __launch_bounds__(256) void k_obs_f32(const uint32_t *__restrict__ obs, float *__restrict__ out,
+                                                 int64_t n, int W, int H) {
+    __shared__ uint32_t O[kWave * kMaxW];
+    const int64_t e0 = (int64_t)blockIdx.x * kWave;
+    const int ne = (int)(n - e0 < kWave ? n - e0 : kWave);
+    for (int i = threadIdx.x; i < W * kWave; i += blockDim.x) {
+        const int x = i / kWave, l = i - x * kWave;
+        if (l < ne) O[l * W + x] = obs[(int64_t)x * n + e0 + l];
+    }
+    __syncthreads();
+    const int per = W * H;
+    const int total = ne * per;  // elements of this block's contiguous region
+    float *base = out + e0 * per;
+    if ((reinterpret_cast<uintptr_t>(base) & 15u) == 0 && (total & 3) == 0) {
+        for (int c = threadIdx.x; 4 * c < total; c += blockDim.x) {
+            int f = 4 * c;
+            int le = f / per, rem = f - le * per;
+            int x = rem / H, y = rem - x * H;
+            float v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                v[j] = (float)((O[le * W + x] >> y) & 1u);
+                if (++y == H) {
+                    y = 0;
+                    if (++x == W) {
+                        x = 0;
+                        ++le;
+                    }
+                }
+            }
+            store16_nt(base + f, v);
+        }
+    } else {
+        for (int f = threadIdx.x; f < total; f += blockDim.x) {
+            const int le = f / per, rem = f - le * per;
+            const int x = rem / H, y = rem - x * H;
+            base[f] = (float)((O[le * W + x] >> y) & 1u);
+        }
     }
 }
 
-// convert_grayscale (tetris_env.py:76-114) in closed form.  The reference
-// transposes the (W, H) board to (H, W), scales each cell to blk x blk, puts
-// `gap` background lines before every block row/column and after the last,
-// then centres the result with border (0) padding.  Pixel (r, c): r runs over
-// board rows y, c over board columns x.  One thread per output pixel.
+// convert_grayscale (tetris_env.py:76-114) [+ the rgb channel repeat, :117-122]
+// in closed form.  The reference transposes the (W, H) board to (H, W),
+// scales each cell to blk x blk, puts `gap` background lines before every
+// block row/column and after the last, then centres the result with border
+// (0) padding.  Image row r maps to board row y, column c to board column x;
+// the two maps (-2 border, -1 background line, else the board index) are
+// tabulated in LDS once per block, so a pixel is two table reads and a bit
+// test: 0 (border), 128 (background), 190 (cell).
 template <typename T>
-__global__ void k_grayscale(const uint32_t *__restrict__ obs, T *__restrict__ out, int64_t n,
-                            int W, int H, int size, int channels) {
+__global__ __launch_bounds__(256) void k_grayscale(const uint32_t *__restrict__ obs, T *__restrict__ out,
+                                                   int64_t n, int W, int H, int size, int channels) {
+    __shared__ uint32_t O[kImgEnvs * kMaxW];
+    __shared__ int8_t RM[kMaxImg], CM[kMaxImg];
+    const int64_t e0 = (int64_t)blockIdx.x * kImgEnvs;
+    const int ne = (int)(n - e0 < kImgEnvs ? n - e0 : kImgEnvs);
     const int lim = W > H ? W : H;
     const int gap = size / 100 + 1;
     const int blk = (size - 2 * gap) / lim - gap;
     const int pitch = blk + gap;
     const int pr = (size - (gap + pitch * H)) / 2;  // padding_width  (axis 0 = y)
     const int pc = (size - (gap + pitch * W)) / 2;  // padding_height (axis 1 = x)
-    const int64_t per = (int64_t)size * size;
-    const int64_t total = n * per;
-    for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < total;
-         f += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t e = f / per;
-        const int pix = (int)(f - e * per);
-        const int r = pix / size - pr;
-        const int c = pix - (pix / size) * size - pc;
-        uint32_t v = 0;  // border_shade
-        if (r >= 0 && c >= 0 && r < gap + pitch * H && c < gap + pitch * W) {
-            v = 128;  // background_shade
-            const int ry = r % pitch, cx = c % pitch;
-            if (ry >= gap && cx >= gap) {
-                const int y = r / pitch, x = c / pitch;
-                if ((obs[(int64_t)x * n + e] >> y) & 1u) v = 190;  // piece_shade
+    for (int i = threadIdx.x; i < size; i += blockDim.x) {
+        const int r = i - pr, c = i - pc;
+        RM[i] = (int8_t)((r < 0 || r >= gap + pitch * H) ? -2 : (r % pitch < gap ? -1 : r / pitch));
+        CM[i] = (int8_t)((c < 0 || c >= gap + pitch * W) ? -2 : (c % pitch < gap ? -1 : c / pitch));
+    }
+    for (int i = threadIdx.x; i < W * kImgEnvs; i += blockDim.x) {
+        const int x = i / kImgEnvs, l = i - x * kImgEnvs;
+        if (l < ne) O[l * kMaxW + x] = obs[(int64_t)x * n + e0 + l];
+    }
+    __syncthreads();
+    const int per = size * size * channels;  // elements per env
+    const int total = ne * per;
+    T *base = out + e0 * per;
+    auto pix = [&](int le, int r, int c) -> T {
+        const int y = RM[r], x = CM[c];
+        const uint32_t v = (y == -2 || x == -2) ? 0u
+                           : (y < 0 || x < 0) ? 128u
+                           : (((O[le * kMaxW + x] >> y) & 1u) ? 190u : 128u);
+        return (T)v;
+    };
+    constexpr int V = 16 / sizeof(T);
+    if ((reinterpret_cast<uintptr_t>(base) & 15u) == 0 && (total % V) == 0) {
+        for (int c0 = threadIdx.x; V * c0 < total; c0 += blockDim.x) {
+            const int f = V * c0;
+            int le = f / per, rem = f - le * per;
+            int p = rem / channels, k = rem - p * channels;
+            int r = p / size, c = p - r * size;
+            T v[V];
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                v[j] = pix(le, r, c);
+                if (++k == channels) {
+                    k = 0;
+                    if (++c == size) {
+                        c = 0;
+                        if (++r == size) {
+                            r = 0;
+                            ++le;
+                        }
+                    }
+                }
             }
+            store16_nt(base + f, v);
         }
-        T *o = out + f * channels;
-        for (int ch = 0; ch < channels; ++ch) o[ch] = (T)v;
+    } else {
+        for (int f = threadIdx.x; f < total; f += blockDim.x) {
+            const int le = f / per, rem = f - le * per;
+            const int p = rem / channels;
+            base[f] = pix(le, p / size, p - (p / size) * size);
+        }
     }
 }
 
@@ -1909,25 +1993,22 @@ hipError_t launch_rollout(const KParams &p, hipStream_t s) {
 }
 
 hipError_t launch_obs_f32(const KParams &p, const uint32_t *obs, float *out, hipStream_t s) {
-    const int64_t total = p.n * p.W * p.H;
-    int64_t blocks = (total + 255) / 256;
-    if (blocks > 65536) blocks = 65536;
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_obs_f32, dim3((unsigned)blocks), dim3(256), 0, s, obs, out, p.n, p.W, p.H);
+    if (p.n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_obs_f32, dim3((unsigned)((p.n + kWave - 1) / kWave)), dim3(256), 0, s, obs, out, p.n,
+                       p.W, p.H);
     return hipGetLastError();
 }
 
 hipError_t launch_grayscale(const KParams &p, const uint32_t *obs, int size, int channels,
                             int as_u8, void *out, hipStream_t s) {
-    const int64_t total = p.n * (int64_t)size * size;
-    int64_t blocks = (total + 255) / 256;
-    if (blocks > 65536) blocks = 65536;
+    if (p.n <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((p.n + kImgEnvs - 1) / kImgEnvs)), block(256);
     if (as_u8)
-        hipLaunchKernelGGL(k_grayscale<uint8_t>, dim3((unsigned)blocks), dim3(256), 0, s, obs,
-                           (uint8_t *)out, p.n, p.W, p.H, size, channels);
+        hipLaunchKernelGGL(k_grayscale<uint8_t>, grid, block, 0, s, obs, (uint8_t *)out, p.n, p.W, p.H, size,
+                           channels);
     else
-        hipLaunchKernelGGL(k_grayscale<float>, dim3((unsigned)blocks), dim3(256), 0, s, obs,
-                           (float *)out, p.n, p.W, p.H, size, channels);
+        hipLaunchKernelGGL(k_grayscale<float>, grid, block, 0, s, obs, (float *)out, p.n, p.W, p.H, size,
+                           channels);
     return hipGetLastError();
 }
 

@@ -248,6 +248,53 @@ def test_grayscale_kernel_matches_reference_images():
             assert np.array_equal(g3, np.repeat(d[key][i][:, :, None], 3, axis=2)), (i, size)
 
 
+def _image_np(cols, W, H, size):
+    """convert_grayscale (tetris_env.py:76-114) per env from packed columns
+    [n][W] (the closed form pinned by test_grayscale_kernel_matches_reference_images)."""
+    lim = max(W, H)
+    gap = size // 100 + 1
+    blk = (size - 2 * gap) // lim - gap
+    pitch = blk + gap
+    pr, pc = (size - (gap + pitch * H)) // 2, (size - (gap + pitch * W)) // 2
+    r = np.arange(size) - pr
+    c = np.arange(size) - pc
+    rin = (r >= 0) & (r < gap + pitch * H)
+    cin = (c >= 0) & (c < gap + pitch * W)
+    rcell = rin & (r % pitch >= gap)
+    ccell = cin & (c % pitch >= gap)
+    y = np.where(rcell, r // pitch, 0)
+    x = np.where(ccell, c // pitch, 0)
+    cols = np.asarray(cols, np.uint64)
+    bits = (cols[:, x][:, None, :] >> y.astype(np.uint64)[None, :, None]) & np.uint64(1)  # [n][r][c]
+    img = np.where(rin[:, None] & cin[None, :], 128, 0)[None].repeat(len(cols), 0)
+    img = np.where((rcell[:, None] & ccell[None, :])[None] & (bits == 1), 190, img)
+    return img
+
+
+@pytest.mark.parametrize("n", [1, 17, 1000])
+def test_image_kernels_ragged_batches(n):
+    """st_grayscale / st_obs_to_f32 over ragged batches (16-env and 64-env
+    blocks with a partial last block), every size / channel / dtype path."""
+    G = _engine()
+    for (W, H) in ((10, 20), (7, 13)):
+        b = G.TetrisBatch(n, width=W, height=H, seeds=range(n), autoreset="same_step")
+        b.reset()
+        for t in range(30):
+            b.step(b.gen_actions(t, 9))
+        cols = b.obs.cpu().numpy().view(np.uint32).T.astype(np.uint64)   # [n][W]
+        f32 = b.obs_to_f32().cpu().numpy()
+        ref = ((cols[:, :, None] >> np.arange(H, dtype=np.uint64)) & 1).astype(np.float32)
+        assert np.array_equal(f32, ref), (W, H)
+        for size in (84, 160, 50):
+            exp = _image_np(cols, W, H, size)
+            for ch in (1, 3):
+                for u8 in (False, True):
+                    g = b.grayscale(b.obs, size, ch, as_u8=u8).cpu().numpy()
+                    assert g.shape == (n, size, size, ch)
+                    assert np.array_equal(g, np.repeat(exp[..., None], ch, axis=3).astype(g.dtype)), \
+                        (W, H, size, ch, u8)
+
+
 # ---------------------------------------------------------------- single-env surface
 @pytest.mark.parametrize("name", ["default", "adv_holes_height", "high_height_holes", "lock2_reset"])
 @pytest.mark.parametrize("rng", ["private", "global"])

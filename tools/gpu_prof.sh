@@ -1,23 +1,28 @@
 #!/bin/bash
-# Profiling pass (run after tools/gpu_check.sh in the same gpurun call or alone):
-#  - rocprofv3 --kernel-trace --stats of a short bench run (all variants)
-#  - PMC: FETCH_SIZE and WRITE_SIZE in SEPARATE passes (TCC slot limits), eager
-#    launches, plus the same two passes over tools/pmc_calib (known byte counts)
-#  - tools/pmc_summary.py -> profiles/${TAG}_pmc.json
+# Profiling pass for one round's numbers (TAG=r02 bash tools/gpu_prof.sh):
+#  1. rocprofv3 --kernel-trace --stats of the default bench command (all
+#     variants) and of the headline alone (--no-extras: clean per-kernel stats),
+#     plus tools/trace_summary.py per-run splits of both traces
+#  2. PMC: FETCH_SIZE and WRITE_SIZE in SEPARATE passes (TCC slot limits) over
+#     eager launches of every variant, plus the same two passes over
+#     tools/pmc_calib (known byte counts) -> tools/pmc_summary.py ->
+#     gpurun_out/${TAG}_pmc.json (copy to profiles/)
+# Every GPU step has its own time limit; steps are chained with &&.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd /tmp && export TMPDIR=/tmp
-TAG=${TAG:-r01}
+TAG=${TAG:-r02}
 O="$R/gpurun_out"
 mkdir -p "$O"
-B="python3 $R/bench.py --no-cpu-baseline"
-# PMC passes: eager launches, all variants (st_step packed/f32, st_rollout packed/f32)
-run() { echo "== $*"; timeout -k 10 300 "$@"; }
-run rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$TAG" -o packed -- $B > "$O/prof_bench_$TAG.json" 2> "$O/prof_$TAG.err" \
- && run rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$O/pmc_fetch_$TAG" -o packed -- $B --steps 600 --warmup 100 --no-graph --rollout-chunk 50 > /dev/null 2>> "$O/prof_$TAG.err" \
- && run rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$O/pmc_write_$TAG" -o packed -- $B --steps 600 --warmup 100 --no-graph --rollout-chunk 50 > /dev/null 2>> "$O/prof_$TAG.err" \
+B="$R/bench.py"
+run() { echo "== $*"; timeout -k 10 400 "$@"; }
+run rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$TAG" -o full -- python3 $B --no-cpu-baseline > "$O/prof_bench_$TAG.json" 2> "$O/prof_$TAG.err" \
+ && run rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$TAG" -o head -- python3 $B --no-extras > "$O/prof_head_$TAG.json" 2>> "$O/prof_$TAG.err" \
+ && run rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$O/pmc_fetch_$TAG" -o packed -- python3 $B --no-cpu-baseline --steps 600 --warmup 100 --launch eager --rollout-chunk 50 > /dev/null 2>> "$O/prof_$TAG.err" \
+ && run rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$O/pmc_write_$TAG" -o packed -- python3 $B --no-cpu-baseline --steps 600 --warmup 100 --launch eager --rollout-chunk 50 > /dev/null 2>> "$O/prof_$TAG.err" \
  && run rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$O/pmc_cal_fetch_$TAG" -o cal -- "$R/tools/pmc_calib" >> "$O/prof_$TAG.err" 2>&1 \
  && run rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$O/pmc_cal_write_$TAG" -o cal -- "$R/tools/pmc_calib" >> "$O/prof_$TAG.err" 2>&1 \
  && (cd "$R" && python3 tools/pmc_summary.py "$TAG" "$O/pmc_fetch_$TAG" "$O/pmc_write_$TAG" "$O/pmc_cal_fetch_$TAG" "$O/pmc_cal_write_$TAG" > "$O/pmc_summary_$TAG.json" && cp "profiles/${TAG}_pmc.json" "$O/") \
- && (cd "$R" && python3 tools/trace_summary.py "$O/prof_$TAG/packed_kernel_trace.csv" > "$O/trace_summary_$TAG.txt") \
+ && (cd "$R" && python3 tools/trace_summary.py "$O/prof_$TAG/full_kernel_trace.csv" > "$O/trace_summary_$TAG.txt" \
+     && python3 tools/trace_summary.py "$O/prof_$TAG/head_kernel_trace.csv" > "$O/trace_summary_head_$TAG.txt") \
  && echo "prof ok"

@@ -9,6 +9,9 @@ factors are measured on tools/pmc_calib.hip's 512 MiB streams with the step
 kernel's own 4 B/lane shapes (factor = true bytes / (counter * 1024)).
 
 usage: pmc_summary.py TAG FETCH_DIR WRITE_DIR CALIB_FETCH_DIR CALIB_WRITE_DIR
+
+The summary carries bench.kernel_source_sha() of the sources it measured;
+bench.py reports `traffic` only from a summary with its own sources' hash.
 """
 import csv
 import glob
@@ -20,13 +23,18 @@ from collections import defaultdict
 CALIB_BYTES = 512 << 20
 
 
-def per_kernel(d, counter):
+def per_kernel(d, counter, by_grid=False):
+    """counter values per kernel name (by_grid: per (name, grid size), so that
+    the bench's 65,536-env and 4,096-env launches of one kernel stay apart)."""
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     vals = defaultdict(list)
     for f in files:
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") == counter:
-                vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+                key = r["Kernel_Name"]
+                if by_grid:
+                    key = (key, int(r.get("Grid_Size") or 0))
+                vals[key].append(float(r["Counter_Value"]))
     return vals
 
 
@@ -50,9 +58,11 @@ def main():
     f_rd4, raw_rd4 = factor(cf, "rd4", "FETCH_SIZE")
     f_rd16, raw_rd16 = factor(cf, "rd16", "FETCH_SIZE")
     f_wr4, raw_wr4 = factor(cw, "wr4", "WRITE_SIZE")
-    fetch = per_kernel(fdir, "FETCH_SIZE")
-    write = per_kernel(wdir, "WRITE_SIZE")
-    out = {"tag": tag,
+    fetch = per_kernel(fdir, "FETCH_SIZE", by_grid=True)
+    write = per_kernel(wdir, "WRITE_SIZE", by_grid=True)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    out = {"tag": tag, "kernel_source_sha": bench.kernel_source_sha(),
            "calibration": {"fetch_factor_4B_lane": f_rd4, "fetch_factor_16B_lane": f_rd16,
                            "write_factor_4B_lane": f_wr4, "raw_kib": {"rd4": raw_rd4, "rd16": raw_rd16,
                                                                      "wr4": raw_wr4},
@@ -68,10 +78,16 @@ def main():
         wk = sum(wv) / len(wv)
         rd = fk * 1024.0 * f_rd4
         wr = wk * 1024.0 * f_wr4
-        out["kernels"][short(k)] = {
-            "launches": len(fv), "fetch_kib": fk, "write_kib": wk,
-            "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
-            "hbm_bytes_per_launch": rd + wr, "full_name": k}
+        name, grid = k
+        ent = {"launches": len(fv), "grid_size": grid, "fetch_kib": fk, "write_kib": wk,
+               "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+               "hbm_bytes_per_launch": rd + wr, "full_name": name}
+        # the largest grid of a kernel (the 65,536-env workloads) under its
+        # short name (bench.load_pmc's key), every grid under name@grid
+        prev = out["kernels"].get(short(name))
+        if prev is None or grid > prev["grid_size"]:
+            out["kernels"][short(name)] = ent
+        out["kernels"][f"{short(name)}@{grid}"] = ent
     os.makedirs("profiles", exist_ok=True)
     path = os.path.join("profiles", f"{tag}_pmc.json")
     json.dump(out, open(path, "w"), indent=1)
