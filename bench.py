@@ -459,6 +459,8 @@ def main():
         variants["c2"]["config"] = f"C2: 4096 boards per GPU, {args.config.upper()} rewards"
         w.close()
         variants.update(image_variants(head, C, timed, roofline, dev, s, sp, W, WU, K))
+        if world == 1:
+            variants["single_env"] = single_env_variant(min(K, 2000))
         if not args.no_clear_heavy and not f32:
             variants["step_clear_heavy"] = clear_heavy(head, cfg_kw, C, ShardedTetris, timed, roofline,
                                                        kname_of, dev, s, sp, rank, world, W, H, K, WU,
@@ -474,6 +476,36 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def single_env_variant(steps: int):
+    """The single-env drop-in (TetrisEnv, tetris_env.py:338-467): wall time
+    per TetrisEnv.step() on uniform random actions with reset on done, numpy
+    obs on the host each step, beside the reference's 30.5 us/step (SURVEY
+    §6, one core of the build container; it cannot run on the GPU box)."""
+    import random
+    from gym_simpletetris_amd.envs.tetris_env import TetrisEnv
+    out = {}
+    rnd = random.Random(1)
+    acts = [rnd.randrange(7) for _ in range(steps + 200)]
+    for obs_type in ("ram", "grayscale"):
+        for rng in ("global", "private"):
+            env = TetrisEnv(obs_type=obs_type, rng=rng, seed=0)
+            env.reset()
+            for a in acts[:200]:
+                if env.step(a)[2]:
+                    env.reset()
+            t0 = time.perf_counter()
+            for a in acts[200:]:
+                if env.step(a)[2]:
+                    env.reset()
+            dt = time.perf_counter() - t0
+            out[f"{obs_type}/{rng}"] = {"us_per_step": dt / steps * 1e6, "steps_per_s": steps / dt}
+            env.close()
+    out["reference_us_per_step"] = {"ram": 1e6 / REF_PY_STEPS_PER_S, "grayscale": 1e6 / 8052,
+                                    "note": "reference TetrisEnv.step(), 1 core of the build container "
+                                            "(SURVEY §6), incl. reset on done"}
+    return out
 
 
 def image_variants(head, C, timed, roofline, dev, s, sp, W, WU, K):

@@ -1701,6 +1701,42 @@ __global__ __launch_bounds__(kWave) void k_render(KParams p) {
         for (int x = 0; x < W; ++x) p.obs[x * p.n + e] = lcol(L, x, lane) & hmask;
 }
 
+// ---------------------------------------------------------------- export
+// st_export_env: one env's outputs and state as one record (the single-env
+// surface's per-step read-back in one transfer): obs words | reward | done |
+// stats rows | MT words.  The MT index row and words are CPython's form,
+// computed read-only the way k_mt_sync rewrites them (the preview's words
+// given back, the generation holding that position): the env keeps its
+// preview and next-generation progress.
+__global__ __launch_bounds__(256) void k_export(KParams p, int64_t env, const uint32_t *obs,
+                                               const int32_t *rew, const uint8_t *done, uint32_t *out) {
+    const int W = p.W;
+    const int words = W + 2 + ST_NSTAT + kMtN;
+    const uint32_t r = (uint32_t)p.stats[(int64_t)ST_STAT_MT_INDEX * p.stride + env];
+    int idx = (int)(r & 0x3FFu);
+    uint32_t cur = (r >> 20) & 1u;
+    if (pv_ok(r)) {  // see k_mt_sync
+        const int c = (int)((r >> 25) & kPvCMax);
+        if (idx > c) {
+            idx -= c;
+        } else {
+            idx = kMtN - (c - idx);
+            cur ^= 1u;
+        }
+    }
+    const uint32_t *g = p.mt + env * kMtPitch + (cur ? kMtB : 0u);
+    for (int i = threadIdx.x; i < words; i += blockDim.x) {
+        uint32_t v;
+        if (i < W) v = obs ? obs[(int64_t)i * p.n + env] : 0u;
+        else if (i == W) v = rew ? (uint32_t)rew[env] : 0u;
+        else if (i == W + 1) v = done ? (uint32_t)done[env] : 0u;
+        else if (i == W + 2 + ST_STAT_MT_INDEX) v = (uint32_t)idx;
+        else if (i < W + 2 + ST_NSTAT) v = (uint32_t)p.stats[(int64_t)(i - W - 2) * p.stride + env];
+        else v = g[i - W - 2 - ST_NSTAT];
+        out[i] = v;
+    }
+}
+
 // ---------------------------------------------------------------- misc
 // Image writers: the output of a block of envs is one contiguous region, so
 // lanes walk it in 16-B chunks (lane-consecutive vector stores, one 1-KB
@@ -2024,6 +2060,12 @@ hipError_t launch_gen_actions(uint8_t *out, int64_t n, int64_t t, uint64_t seed,
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_gen_actions, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, out, n,
                        t, seed, off);
+    return hipGetLastError();
+}
+
+hipError_t launch_export(const KParams &p, int64_t env, const uint32_t *obs, const int32_t *rew,
+                         const uint8_t *done, uint32_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_export, dim3(1), dim3(256), 0, s, p, env, obs, rew, done, out);
     return hipGetLastError();
 }
 

@@ -41,6 +41,18 @@ def _obs_space(obs_type, width, height, extend_dims):
     return spaces.Box(0, 1, shape=shape, dtype=np.float32)
 
 
+def _mapped(t: torch.Tensor):
+    """Device address of a pinned host tensor (hipHostGetDevicePointer), or
+    None if the runtime does not map it for the device."""
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        dp = ctypes.c_void_p()
+        rc = hip.hipHostGetDevicePointer(ctypes.byref(dp), ctypes.c_void_p(t.data_ptr()), 0)
+        return dp if rc == 0 and dp.value else None
+    except OSError:
+        return None
+
+
 class TetrisEnv:
     metadata = {"render.modes": ["human", "rgb_array"], "render_fps": 8}  # :339
 
@@ -79,12 +91,31 @@ class TetrisEnv:
         self._stats = None         # last downloaded counters (host int64 [NSTAT])
         self._started = False
         self._rng_sync_state = None
-        self._piece, self._piece_dirty = 0, True
         dev = self.engine.device
-        self._d_act = torch.zeros(1, dtype=torch.uint8, device=dev)
-        self._h_stats = np.zeros((C.NSTAT, self.engine.stride), np.int32)
+        L = self.engine._L
+        # per-step plumbing without per-call allocations: one device tensor per
+        # action value, the step's outputs, and ONE read-back record
+        # (st_export_env: obs words | reward | done | counters | MT words) plus
+        # the image for grayscale / rgb, copied into pinned host buffers and
+        # waited for once
+        self._acts = [torch.full((1,), a, dtype=torch.uint8, device=dev) for a in range(7)]
+        self._p_acts = [ctypes.c_void_p(t.data_ptr()) for t in self._acts]
+        self._nrec = int(L.st_export_words(width))
+        self._d_rec = torch.empty(self._nrec, dtype=torch.int32, device=dev)
+        self._h_rec = torch.empty(self._nrec, dtype=torch.int32, pin_memory=True)
+        self._h_rec_np = self._h_rec.numpy()
+        self._zeros = torch.zeros((width, 1), dtype=torch.int32, device=dev)
+        self._ch = 1 if obs_type == "grayscale" else 3
+        if obs_type in ("grayscale", "rgb"):
+            self._d_img = torch.empty((1, 84, 84, self._ch), dtype=torch.float32, device=dev)
+            self._h_img = torch.empty((1, 84, 84, self._ch), dtype=torch.float32, pin_memory=True)
         self._h_mt = np.zeros(C.MT_N, np.uint32)
         self._h_idx = np.zeros(1, np.int32)
+        self._yb = np.arange(height, dtype=np.uint32)
+        # the export and image kernels write straight into the pinned buffers
+        # when the runtime maps them for the device (else: device buffer + copy)
+        self._rec_dst = _mapped(self._h_rec)
+        self._img_dst = _mapped(self._h_img) if obs_type in ("grayscale", "rgb") else None
 
     # ------------------------------------------------------------- RNG mirror
     def seed(self, seed=None):
@@ -116,34 +147,51 @@ class TetrisEnv:
         C.check(L.st_copy(ctypes.c_void_p(v.stats + C.STAT["mt_index"] * v.stride * 4),
                           ctypes.c_void_p(self._h_idx.ctypes.data), 4, s))
 
-    def _pull(self, prev_idx=None):
-        """Download the counters; in 'global' mode write the env's MT state
-        back into CPython's random if this call drew pieces."""
-        v = self.engine._views
-        L = self.engine._L
+    def _readback(self, obs_ptr, rew_ptr, done_ptr, prev_idx=None):
+        """One read-back per call: the env's record (st_export_env: outputs,
+        counters and CPython's form of its MT state) and, for image
+        observations, its image, each copied to pinned host memory on the
+        stream, then ONE synchronize.  In 'global' mode CPython's random takes
+        the env's MT state if this call drew pieces.  Returns (obs words u32 [W], reward, done, counters int64
+        [NSTAT], image or None)."""
+        eng = self.engine
+        L, ctx = eng._L, eng._ctx
         s = self._stream()
-        if self._rng_mode == "global":  # CPython's random mirrors the env's MT state
-            self.engine.sync_mt()
-        C.check(L.st_copy(ctypes.c_void_p(self._h_stats.ctypes.data), ctypes.c_void_p(v.stats),
-                          self._h_stats.nbytes, s))
-        torch.cuda.current_stream(self.engine.device).synchronize()
-        st = self._h_stats[:, 0].astype(np.int64)
+        if self._rec_dst is not None:
+            C.check(L.st_export_env(ctx, 0, obs_ptr, rew_ptr, done_ptr, self._rec_dst, s))
+        else:
+            C.check(L.st_export_env(ctx, 0, obs_ptr, rew_ptr, done_ptr, ctypes.c_void_p(self._d_rec.data_ptr()), s))
+            C.check(L.st_copy(ctypes.c_void_p(self._h_rec.data_ptr()), ctypes.c_void_p(self._d_rec.data_ptr()),
+                              self._nrec * 4, s))
+        img = None
+        if self.obs_type in ("grayscale", "rgb"):
+            src = obs_ptr if obs_ptr is not None else ctypes.c_void_p(self._zeros.data_ptr())
+            if self._img_dst is not None:
+                C.check(L.st_grayscale(ctx, src, 84, self._ch, 0, self._img_dst, s))
+            else:
+                C.check(L.st_grayscale(ctx, src, 84, self._ch, 0, ctypes.c_void_p(self._d_img.data_ptr()), s))
+                C.check(L.st_copy(ctypes.c_void_p(self._h_img.data_ptr()), ctypes.c_void_p(self._d_img.data_ptr()),
+                                  self._d_img.numel() * 4, s))
+        torch.cuda.current_stream(eng.device).synchronize()
+        rec = self._h_rec_np
+        W = self.width
+        words = rec[:W].view(np.uint32).copy()
+        st = rec[W + 2: W + 2 + C.NSTAT].astype(np.int64)
         if self._rng_mode == "global":
             idx = int(st[C.STAT["mt_index"]])
             if prev_idx is None or idx != prev_idx or self._rng_sync_state is None:
-                C.check(L.st_copy(ctypes.c_void_p(self._h_mt.ctypes.data), ctypes.c_void_p(v.mt),
-                                  C.MT_N * 4, s))
-                torch.cuda.current_stream(self.engine.device).synchronize()
+                mt = rec[W + 2 + C.NSTAT:].view(np.uint32)
                 old = random.getstate()
-                random.setstate((old[0], tuple(int(w) for w in self._h_mt) + (idx,), old[2]))
+                random.setstate((old[0], tuple(mt.tolist()) + (idx,), old[2]))
             self._rng_sync_state = random.getstate()
-        return st
+        if img is None and self.obs_type in ("grayscale", "rgb"):
+            img = self._h_img.numpy()[0].copy()
+        return words, int(rec[W]), bool(rec[W + 1]), st, img
 
     # ------------------------------------------------------------- gym API
     def _get_info(self, st):
         """TetrisEngine.get_info (tetris_env.py:232-241)."""
-        pw = int(self.engine.get_state(("piece",))["piece"][0]) if self._piece_dirty else self._piece
-        self._piece, self._piece_dirty = pw, False
+        pw = int(st[C.STAT["piece"]]) & 0xFFFFFFFF
         c0 = C.STAT["count0"]
         return {"time": int(st[C.STAT["time"]]),
                 "current_piece": SHAPE_NAMES[pw & 7],
@@ -153,17 +201,15 @@ class TetrisEnv:
                 "deaths": int(st[C.STAT["deaths"]]),
                 "statistics": {SHAPE_NAMES[i]: int(st[c0 + i]) for i in range(7)}}
 
-    def _observation(self, packed: torch.Tensor):
-        """TetrisEnv._observation (tetris_env.py:413-433) + float32 cast."""
+    def _observation(self, words, img):
+        """TetrisEnv._observation (tetris_env.py:413-433) + float32 cast, from
+        the read-back's packed obs words (ram) or image (grayscale / rgb)."""
         if self.obs_type == "ram":
-            out = self.engine.obs_to_f32(packed)[0]
-            obs = out.cpu().numpy()
+            obs = ((words[:, None] >> self._yb[None, :]) & 1).astype(np.float32)
             return obs.reshape(self.width, self.height, 1) if self.extend_dims else obs
-        g = self.engine.grayscale(packed, 84, 1 if self.obs_type == "grayscale" else 3)[0]
-        obs = g.cpu().numpy()
         if self.obs_type == "grayscale":
-            return obs if self.extend_dims else obs.reshape(84, 84)
-        return obs
+            return img if self.extend_dims else img.reshape(84, 84)
+        return img
 
     def _typed_reward(self, r: int, done: bool, prev, st):
         """Reproduce the Python type the reference's reward ends up with (R18)."""
@@ -190,15 +236,12 @@ class TetrisEnv:
             raise KeyError(action)  # value_action_map[action], tetris_env.py:245
         prev = self._stats
         self._push_rng()
-        self._d_act.fill_(int(action))
-        packed, rew, done = self.engine.step(self._d_act, obs="packed")
-        obs = self._observation(packed)
-        r = int(rew[0].item())
-        d = bool(done[0].item())
-        st = self._pull(int(prev[C.STAT["mt_index"]]))
+        eng = self.engine
+        po, pr, pd = (ctypes.c_void_p(t.data_ptr()) for t in (eng.obs, eng.reward, eng.done))
+        C.check(eng._L.st_step(eng._ctx, self._p_acts[int(action)], po, pr, pd, self._stream()))
+        words, r, d, st, img = self._readback(po, pr, pd, int(prev[C.STAT["mt_index"]]))
         self._stats = st
-        self._piece_dirty = True
-        return obs, self._typed_reward(r, d, prev, st), d, self._get_info(st)
+        return self._observation(words, img), self._typed_reward(r, d, prev, st), d, self._get_info(st)
 
     def reset(self, return_info=False):
         """TetrisEnv.reset (tetris_env.py:405-411): clear(); obs is the empty
@@ -206,11 +249,9 @@ class TetrisEnv:
         self._push_rng()
         self.engine.reset()
         self._started = True
-        st = self._pull()
+        words, _, _, st, img = self._readback(ctypes.c_void_p(self._zeros.data_ptr()), None, None)
         self._stats = st
-        self._piece_dirty = True
-        zeros = torch.zeros((self.width, 1), dtype=torch.int32, device=self.engine.device)
-        obs = self._observation(zeros)
+        obs = self._observation(words, img)
         return (obs, self._get_info(st)) if return_info else obs
 
     def render(self, mode="human"):
