@@ -223,8 +223,14 @@ def main():
     dev_idx = 0 if shared else local_rank
     torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx)
-    if world > 1:
+    # ST_BENCH_FORCE_DIST=1 (tests only): the torch.distributed path (RCCL with
+    # the nccl backend) even at one rank, so a one-GPU box runs its calls
+    use_dist = world > 1 or os.environ.get("ST_BENCH_FORCE_DIST") == "1"
+    if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -246,11 +252,11 @@ def main():
 
     def sync_all():
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if use_dist:
             dist.barrier()
 
     def max_over_ranks(x: float) -> float:
-        if world == 1:
+        if not use_dist:
             return x
         if args.backend == "nccl":
             t = torch.tensor([x], dtype=torch.float64, device=dev)
@@ -466,14 +472,14 @@ def main():
                                                        kname_of, dev, s, sp, rank, world, W, H, K, WU,
                                                        aseed, args.config, args.launch)
         out["variants"] = variants
-        if world > 1:
+        if use_dist:
             out["gather_variant"] = gather_variant(head, args, C, output_buffer, buffer_views,
                                                    dev, s, sp, rank, world, W, WU, max_over_ranks)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.config)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -99,3 +99,19 @@ def test_bench_gpus2_direct_invocation():
     assert d["n_gpus"] == 2 and d["config"]["envs_total"] == 2 * 8192
     assert d["value"] > 0 and d["gather_variant"]["steps"] == 20
     assert d["scaling"] == "weak"
+
+
+def test_bench_rccl_calls_one_rank():
+    """The nccl (RCCL) side of bench.py on a one-GPU box: init with device_id,
+    barriers, the MAX all-reduce of the timings and the double-buffered async
+    gather, at one rank (two ranks cannot share a GPU under RCCL)."""
+    env = dict(os.environ, ST_BENCH_FORCE_DIST="1", RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--backend", "nccl",
+                        "--steps", "30", "--warmup", "5", "--n-envs", "8192", "--no-cpu-baseline",
+                        "--no-clear-heavy", "--gather-steps", "20"],
+                       env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["gather_variant"]["backend"] == "nccl" and d["gather_variant"]["steps"] == 20
+    assert d["value"] > 0
