@@ -811,11 +811,13 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
     constexpr bool BUILD = ROLE != kRoleL;
     uint32_t tab_m = 0, tab_g = 0;
     if constexpr (BUILD) {
+        // one v_writelane per entry (the constant in an SGPR: SALU): 56 VALU
+        // instead of a compare + two selects per entry (~140 VALU), on the
+        // draw wave's path to B0
 #pragma unroll
         for (int i = 0; i < 28; ++i) {
-            const bool me = lane == i;
-            tab_m = me ? kTab.m[i] : tab_m;
-            tab_g = me ? kTab.g[i] : tab_g;
+            asm("v_writelane_b32 %0, %1, %2" : "+v"(tab_m) : "s"(kTab.m[i]), "i"(i));
+            asm("v_writelane_b32 %0, %1, %2" : "+v"(tab_g) : "s"(kTab.g[i]), "i"(i));
         }
     }
     const int lrow = lane >> 4, lcc = 4 * (lane & 15);  // this lane's row-in-group, env slot
