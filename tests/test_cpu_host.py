@@ -147,3 +147,27 @@ def test_algorithmic_bytes_formula():
     assert b == (1 + 4 + 4 + 40) + (4 + 4 + 4 + 1 + 40)
     assert bench.algorithmic_bytes(10, 20, 0.0, True) == b + 800
     assert bench.algorithmic_bytes(10, 20, 1.0, False) > b
+
+
+def test_bench_roofline_bytes_and_pmc_tie():
+    import json
+    import bench
+    assert bench.s8d_bytes(0.0, False) == 182 and bench.s8d_bytes(1.0, False) == 366
+    assert bench.s8d_bytes(0.5, True) == 902 + 92
+    assert abs(bench.algorithmic_bytes(10, 20, 1.0, False) - (102 + 167.7)) < 1e-9
+    # traffic is taken only from a PMC summary of the same kernel sources
+    pmc = os.path.join(ROOT, "profiles", "r02_pmc.json")
+    d = json.load(open(pmc))
+    kname = "k_step<10, 20, false, false, true>"
+    got, src = bench.load_pmc(kname, d["kernel_source_sha"])
+    assert src == "r02_pmc.json" and got == d["kernels"][kname]["hbm_bytes_per_launch"]
+    got, why = bench.load_pmc(kname, "0" * 16)
+    assert got is None and "no PMC pass" in why
+    assert len(bench.kernel_source_sha()) == 16
+
+
+def test_bench_cpu_baseline_all_cores():
+    import bench
+    cb = bench.cpu_baseline(0.2, "c4")
+    assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0 and cb["single_core"] > 0
+    assert cb["nproc"] >= 1 and cb["cpu_model"]
