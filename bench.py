@@ -100,10 +100,17 @@ def kernel_source_sha() -> str:
     return h.hexdigest()[:16]
 
 
+def step_grid(n: int) -> int:
+    """Grid size in threads of k_step / k_rollout for n envs (128 per 64 envs),
+    the key tools/pmc_summary.py files a launch under (`name@grid`)."""
+    return (n + 63) // 64 * 128
+
+
 def load_pmc(kname: str, sha: str):
     """Per-launch HBM bytes (FETCH+WRITE, gfx950-corrected by
-    tools/pmc_summary.py) of `kname` from a committed profiles/*_pmc.json whose
-    kernel-source hash equals the running sources'; (None, reason) if none."""
+    tools/pmc_summary.py) of `kname` (`name@grid`: that kernel at that grid
+    size) from a committed profiles/*_pmc.json whose kernel-source hash equals
+    the running sources'; (None, reason) if none."""
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), reverse=True):
         try:
             d = json.load(open(f))
@@ -306,10 +313,13 @@ def main():
             return f"k_step<10, 20, {b(f32)}, false, {b(sc0)}>"
         return f"k_rollout<10, 20, {b(f32)}, {b(sc0)}>"
 
-    def roofline(kern_us, bpe, units_per_launch, kname, extra=None):
+    def roofline(kern_us, bpe, units_per_launch, kname, extra=None, grid=None):
         bpl = bpe * units_per_launch
         achieved = bpl / (kern_us * 1e-6) / 1e9
-        traffic, src = load_pmc(kname, sha)
+        if grid is None:
+            traffic, src = None, "not collected for this variant"
+        else:
+            traffic, src = load_pmc(f"{kname}@{grid}", sha)
         r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
              "kernel_us": kern_us, "bytes_per_env_step": bpe, "bytes_per_launch": bpl,
@@ -369,7 +379,8 @@ def main():
             del keep
             kern_us = ev_ms * 1e3 / K
             kname = kname_of("step", self.f32, self.sc0)
-            rl = roofline(kern_us, s8d_bytes(p_lock, self.f32), self.n_local, kname, {
+            rl = roofline(kern_us, s8d_bytes(p_lock, self.f32), self.n_local, kname, grid=step_grid(self.n_local),
+                          extra={
                 "bytes_formula": "SURVEY 8(d): %d + 184 p_lock" % (902 if self.f32 else 182),
                 "frac_s8d": s8d_bytes(p_lock, self.f32) * self.n_local / (kern_us * 1e3) / HBM_PEAK_GBS,
                 "bytes_per_env_step_layout": algorithmic_bytes(W, H, p_lock, self.f32),
@@ -450,7 +461,7 @@ def main():
                 "value": head.n_global * nch * CH / el, "ms_per_step": el / (nch * CH) * 1e3,
                 "steps_per_launch": CH, "p_lock": pl,
                 "roofline": roofline(kern_us, rollout_bytes(W, H, pl, use_f32, CH), CH * n_local,
-                                     kname_of("rollout", use_f32, head.sc0),
+                                     kname_of("rollout", use_f32, head.sc0), grid=step_grid(n_local), extra=
                                      {"bytes_formula": "rollout: I/O per step + state r/w per launch / K",
                                       "p_lock": pl})}
             del rf
@@ -604,7 +615,7 @@ def clear_heavy(head, cfg_kw, C, ShardedTetris, timed, roofline, kname_of, dev, 
     r = {"value": n_global * K / el, "ms_per_step": el / K * 1e3, "p_lock": pl,
          "lines_per_env_step": (n_cleared / 100.0 / (ce.n * K)) if config == "c3" else None,
          "actions": "st_policy_greedy (greedy placement, 3% uniform), recorded then replayed",
-         "roofline": roofline(kern_us, bpe, ce.n, kname_of("step", False, not cfg_kw),
+         "roofline": roofline(kern_us, bpe, ce.n, kname_of("step", False, not cfg_kw), grid=step_grid(ce.n), extra=
                               {"bytes_formula": "SURVEY 8(d): 182 + 184 p_lock", "p_lock": pl})}
     del g
     ce.close()

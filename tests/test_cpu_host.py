@@ -158,9 +158,10 @@ def test_bench_roofline_bytes_and_pmc_tie():
     # traffic is taken only from a PMC summary of the same kernel sources
     pmc = os.path.join(ROOT, "profiles", "r02_pmc.json")
     d = json.load(open(pmc))
-    kname = "k_step<10, 20, false, false, true>"
+    kname = "k_step<10, 20, false, false, true>@%d" % bench.step_grid(65536)
     got, src = bench.load_pmc(kname, d["kernel_source_sha"])
     assert src == "r02_pmc.json" and got == d["kernels"][kname]["hbm_bytes_per_launch"]
+    assert bench.step_grid(4096) == 8192 and bench.step_grid(65536) == 131072
     got, why = bench.load_pmc(kname, "0" * 16)
     assert got is None and "no PMC pass" in why
     assert len(bench.kernel_source_sha()) == 16
