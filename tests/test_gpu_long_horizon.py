@@ -193,3 +193,48 @@ def test_bench_workload_st_rollout(config):
     finally:
         orc.close()
         eng.close()
+
+
+@pytest.mark.parametrize("n,steps", [(65537, 600), (1 << 20, 24)])
+def test_ragged_and_large_batches(n, steps):
+    """A ragged batch (65,537 envs: the last wave holds one real env, the
+    stride is padded) over 600 graph-replayed steps, and 2^20 envs (16x the
+    headline batch) over 24 steps, both bit-exact vs the oracle, C4 scoring."""
+    import gym_simpletetris_amd as G
+    from gym_simpletetris_amd import _lib as C
+    dev = torch.device("cuda", 0)
+    kw = CONFIGS["c4"]
+    eng = G.TetrisBatch(n, autoreset="same_step", seeds=[SEED_BASE + e for e in range(n)],
+                        device=dev, width=W, height=H, **kw)
+    acts = torch.empty((steps, n), dtype=torch.uint8, device=dev)
+    for t in range(steps):
+        eng.gen_actions(t, ASEED, out=acts[t])
+    eng.reset()
+    obs = torch.empty((steps, W, n), dtype=torch.int32, device=dev)
+    rew = torch.empty((steps, n), dtype=torch.int32, device=dev)
+    done = torch.empty((steps, n), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+    L, ctx = eng._L, eng._ctx
+    s = torch.cuda.Stream(dev)
+    sp = ctypes.c_void_p(s.cuda_stream)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        for t in range(steps):
+            C.check(L.st_step(ctx, ctypes.c_void_p(acts[t].data_ptr()), ctypes.c_void_p(obs[t].data_ptr()),
+                              ctypes.c_void_p(rew[t].data_ptr()), ctypes.c_void_p(done[t].data_ptr()), sp))
+    with torch.cuda.stream(s):
+        g.replay()
+    torch.cuda.synchronize(dev)
+    del g
+    orc = ParallelOracle(n, kw)
+    try:
+        CH = 100
+        for t0 in range(0, steps, CH):
+            T = min(CH, steps - t0)
+            ref = orc.rollout(t0, T)
+            _compare(t0, rew[t0:t0 + T].cpu().numpy(), done[t0:t0 + T].cpu().numpy(),
+                     obs[t0:t0 + T].cpu().numpy().view(np.uint32), ref)
+        _check_final(eng, orc)
+    finally:
+        orc.close()
+        eng.close()
