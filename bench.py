@@ -550,7 +550,7 @@ def image_variants(head, C, timed, roofline, dev, s, sp, W, WU, K):
         kern_us = ev * 1e3 / KG
         bpe = 4 * W + 84 * 84 * ch * 4
         r = {"kernel_only": True, "launches": KG, "kernel_us": kern_us,
-             "roofline": roofline(kern_us, bpe, n, "k_grayscale<float>",
+             "roofline": roofline(kern_us, bpe, n, "k_grayscale<float, 1>",
                                   {"bytes_formula": f"read packed obs 4W + write 84*84*{ch}*4 per env"})}
         # whole steps with this obs_type: st_step + the image per step
         KS = max(1, min(K, 100))

@@ -1808,9 +1808,10 @@ __global__ __launch_bounds__(256) void k_obs_f32(const uint32_t *__restrict__ ob
 // the two maps (-2 border, -1 background line, else the board index) are
 // tabulated in LDS once per block, so a pixel is two table reads and a bit
 // test: 0 (border), 128 (background), 190 (cell).
-template <typename T>
+template <typename T, int CH>
 __global__ __launch_bounds__(256) void k_grayscale(const uint32_t *__restrict__ obs, T *__restrict__ out,
-                                                   int64_t n, int W, int H, int size, int channels) {
+                                                   int64_t n, int W, int H, int size) {
+    constexpr int channels = CH;
     __shared__ uint32_t O[kImgEnvs * kMaxW];
     __shared__ int8_t RM[kMaxImg], CM[kMaxImg];
     const int64_t e0 = (int64_t)blockIdx.x * kImgEnvs;
@@ -1841,29 +1842,56 @@ __global__ __launch_bounds__(256) void k_grayscale(const uint32_t *__restrict__ 
                            : (((O[le * kMaxW + x] >> y) & 1u) ? 190u : 128u);
         return (T)v;
     };
-    constexpr int V = 16 / sizeof(T);
+    // A thread writes one 16-B chunk per iteration, lane-consecutive (48-B
+    // lane strides -- a thread taking an rgb period of 3 chunks -- measured 5x
+    // slower).  Gray (CH == 1): a chunk is V whole pixels, each decoded once.
+    // RGB: the chunk's elements are decoded one by one (decoding only where a
+    // new pixel starts measured slower: divergent LDS reads).  The position
+    // advances by the block's stride through block-uniform digits: no
+    // runtime division in the loop.
+    constexpr int V = 16 / (int)sizeof(T);  // elements per chunk
     if ((reinterpret_cast<uintptr_t>(base) & 15u) == 0 && (total % V) == 0) {
-        for (int c0 = threadIdx.x; V * c0 < total; c0 += blockDim.x) {
-            const int f = V * c0;
-            int le = f / per, rem = f - le * per;
-            int p = rem / channels, k = rem - p * channels;
-            int r = p / size, c = p - r * size;
+        const int S = (int)blockDim.x * V;  // elements per block iteration
+        const int sk = S % channels, sp = S / channels;
+        const int sc = sp % size, sr = (sp / size) % size, sl = sp / (size * size);
+        int f = V * (int)threadIdx.x;
+        int le = f / per, rem = f - le * per;
+        int pp = rem / channels, k = rem - pp * channels;
+        int r = pp / size, c = pp - r * size;
+        for (; f < total; f += S) {
             T v[V];
+            int jk = k, jc = c, jr = r, jl = le;
 #pragma unroll
             for (int j = 0; j < V; ++j) {
-                v[j] = pix(le, r, c);
-                if (++k == channels) {
-                    k = 0;
-                    if (++c == size) {
-                        c = 0;
-                        if (++r == size) {
-                            r = 0;
-                            ++le;
+                v[j] = pix(jl, jr, jc);
+                if (CH == 1 || ++jk == channels) {
+                    jk = 0;
+                    if (++jc == size) {
+                        jc = 0;
+                        if (++jr == size) {
+                            jr = 0;
+                            ++jl;
                         }
                     }
                 }
             }
             store16_nt(base + f, v);
+            k += sk;
+            if (k >= channels) {
+                k -= channels;
+                ++c;
+            }
+            c += sc;
+            if (c >= size) {
+                c -= size;
+                ++r;
+            }
+            r += sr;
+            if (r >= size) {
+                r -= size;
+                ++le;
+            }
+            le += sl;
         }
     } else {
         for (int f = threadIdx.x; f < total; f += blockDim.x) {
@@ -2041,12 +2069,14 @@ hipError_t launch_grayscale(const KParams &p, const uint32_t *obs, int size, int
                             int as_u8, void *out, hipStream_t s) {
     if (p.n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((p.n + kImgEnvs - 1) / kImgEnvs)), block(256);
-    if (as_u8)
-        hipLaunchKernelGGL(k_grayscale<uint8_t>, grid, block, 0, s, obs, (uint8_t *)out, p.n, p.W, p.H, size,
-                           channels);
+    if (as_u8 && channels == 3)
+        hipLaunchKernelGGL((k_grayscale<uint8_t, 3>), grid, block, 0, s, obs, (uint8_t *)out, p.n, p.W, p.H, size);
+    else if (as_u8)
+        hipLaunchKernelGGL((k_grayscale<uint8_t, 1>), grid, block, 0, s, obs, (uint8_t *)out, p.n, p.W, p.H, size);
+    else if (channels == 3)
+        hipLaunchKernelGGL((k_grayscale<float, 3>), grid, block, 0, s, obs, (float *)out, p.n, p.W, p.H, size);
     else
-        hipLaunchKernelGGL(k_grayscale<float>, grid, block, 0, s, obs, (float *)out, p.n, p.W, p.H, size,
-                           channels);
+        hipLaunchKernelGGL((k_grayscale<float, 1>), grid, block, 0, s, obs, (float *)out, p.n, p.W, p.H, size);
     return hipGetLastError();
 }
 
