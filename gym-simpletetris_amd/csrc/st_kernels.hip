@@ -802,12 +802,11 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         pw_d = p.piece[e];
         tm_d = reinterpret_cast<const uint32_t *>(p.stats)[(int64_t)ST_STAT_TIME * sd + e];
     }
-    // The piece table, lane i = entry i, from immediates by compare/select
-    // (VALU under the load latency; no memory access: a __constant__ load
-    // gets sunk by the compiler past the state loads' completion -- one more
-    // serialized round trip -- and inline asm here makes the register
-    // allocator spill the in-flight state loads to scratch).  Two waves: the
-    // draw wave builds it (and the walls, and the f32 nibble table).
+    // The piece table, lane i = entry i, from immediates (under the load
+    // latency; no memory access: a __constant__ load gets sunk by the
+    // compiler past the state loads' completion -- one more serialized round
+    // trip).  Two waves: the draw wave builds it (and the walls, and the f32
+    // nibble table).
     constexpr bool BUILD = ROLE != kRoleL;
     uint32_t tab_m = 0, tab_g = 0;
     if constexpr (BUILD) {
