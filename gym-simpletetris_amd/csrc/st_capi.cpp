@@ -22,7 +22,6 @@ struct st_ctx {
     uint32_t *piece;
     int32_t *stats;
     uint32_t *mt;
-    uint32_t *mtc;
 };
 
 namespace {
@@ -76,7 +75,6 @@ st::KParams params(const st_ctx *c) {
     p.piece = c->piece;
     p.stats = c->stats;
     p.mt = c->mt;
-    p.mtc = c->mtc;
     return p;
 }
 
@@ -84,10 +82,9 @@ void free_state(st_ctx *c) {
     if (c->board) (void)hipFree(c->board);
     if (c->stats) (void)hipFree(c->stats);
     if (c->mt) (void)hipFree(c->mt);
-    if (c->mtc) (void)hipFree(c->mtc);
     if (c->stamps) (void)hipFree(c->stamps);
     c->stamps = nullptr;
-    c->board = c->piece = c->mt = c->mtc = nullptr;
+    c->board = c->piece = c->mt = nullptr;
     c->stats = nullptr;
 }
 
@@ -134,7 +131,6 @@ int st_create(st_ctx **out, const st_config *cfg, int device, int64_t n_envs) {
     // MT states: [stride][kMtPitch] (+ the back pad a draw window may reach)
     if (e == hipSuccess) e = hipMalloc(&c->mt, (sd * st::kMtPitch + st::kMtPadBack) * sizeof(uint32_t));
     // per-env 4-word draw-window cache, valid only where the MT word says so
-    if (e == hipSuccess) e = hipMalloc(&c->mtc, sd * 4 * sizeof(uint32_t));
     if (e == hipSuccess && getenv("ST_STAMPS"))
         e = hipMalloc(&c->stamps, (sd / st::kWave) * st::kStampWords * sizeof(uint64_t));
     if (e != hipSuccess) {

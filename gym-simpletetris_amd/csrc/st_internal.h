@@ -44,7 +44,6 @@ struct KParams {
     uint32_t *piece;    // [stride]
     int32_t *stats;     // [ST_NSTAT][stride]
     uint32_t *mt;       // [stride][kMtPitch]
-    uint32_t *mtc;      // [stride][4] draw-window cache (see st_kernels.hip, MT word)
     // io
     const uint8_t *actions;  // [n]
     const uint8_t *mask;     // [n] (reset) or null

@@ -285,16 +285,17 @@ __device__ __forceinline__ uint32_t mt_pack(int idx, int pg, int cur) {
 }
 // The preview (the piece the env's NEXT spawn takes, drawn one spawn ahead so
 // that no step waits on a draw; see run_steps) in the upper bits of the same
-// word: pv << 21 | ok << 24 | c << 25 | cv << 31, c = the MT words its draw
+// word: pv << 21 | ok << 24 | c << 25, c = the MT words its draw
 // consumed (6 bits; a draw of > 62 words has p < 2^-62), so the reference's
 // state -- the one before the preview was drawn -- is c words back
 // (k_mt_sync).  ok = 0 (a host-written or synced state): the next spawn draws
-// its piece first, then the preview.  cv: the env's 4-word draw-window cache
-// (KParams::mtc) holds words idx..idx+3 of the current generation.
+// its piece first, then the preview.  Bit 31 is zero.  (Round 1 kept a
+// 4-word draw-window cache per env flagged there; with the 64-word successor
+// chunks the draw wave's window wait is off the critical chain, and the
+// cache's 16 B per env and step bought nothing: removed, A/B +-0.)
 constexpr uint32_t kMtLow = (1u << 21) - 1u;  // idx | pg | cur
 constexpr uint32_t kPvOk = 1u << 24;
 constexpr uint32_t kPvCMax = 63u;
-constexpr uint32_t kCv = 1u << 31;
 __device__ __forceinline__ uint32_t mt_keep(uint32_t hi, uint32_t low) { return (hi & ~kMtLow) | low; }
 __device__ __forceinline__ int pv_id(uint32_t r) { return (int)((r >> 21) & 7u); }
 __device__ __forceinline__ bool pv_ok(uint32_t r) { return (r & kPvOk) != 0u; }
@@ -305,10 +306,9 @@ __device__ __forceinline__ uint32_t mt_consumed(uint32_t before, uint32_t after)
     const int c = ((before ^ after) >> 20) & 1u ? kMtN - i0 + i1 : i1 - i0;
     return (uint32_t)c < kPvCMax ? (uint32_t)c : kPvCMax;
 }
-__device__ __forceinline__ uint32_t pv_pack(uint32_t mt_after, int pv, uint32_t c, bool cv = false) {
-    return (mt_after & kMtLow) | ((uint32_t)pv << 21) | kPvOk | (c << 25) | (cv ? kCv : 0u);
+__device__ __forceinline__ uint32_t pv_pack(uint32_t mt_after, int pv, uint32_t c) {
+    return (mt_after & kMtLow) | ((uint32_t)pv << 21) | kPvOk | (c << 25);
 }
-__device__ __forceinline__ bool cache_ok(uint32_t r) { return (r & (kPvOk | kCv)) == (kPvOk | kCv); }
 
 // The wave's 64 MT states as one buffer resource.  Loads and stores of lanes
 // (or operands) not wanted get an out-of-range offset (loads read 0), so each
@@ -329,22 +329,22 @@ __device__ __forceinline__ u32x4 mt_ld16(const MtRes &rs, bool on, uint32_t word
     return __builtin_amdgcn_raw_buffer_load_b128(rs.r, on ? rs.lane_off + 4u * word : kOff, 0, 0);
 }
 
-// The draw window: MT words cur[idx + woff ..] of a locking lane, loaded
+// The draw window: MT words cur[idx ..] of a locking lane, loaded
 // right after the lock decision and consumed by the draw.  Reads past an
 // env's state land in the next env's state or the allocation's back pad.
 struct MtPre {
     uint32_t w[kMtWin];
 };
-// WIN = 8 for st_step (after its 4-word draw-window cache: 12 words before a
-// dependent load, P(12 rejections) <= 2^-12); 16 in rollouts (no cache).
+// WIN = 8 for st_step (P(8 rejections) <= 2^-8: a dependent load for a few
+// lanes per step, off the critical chain); 16 in rollouts.
 template <int WIN>
-__device__ __forceinline__ void mt_pre_load(const MtRes &rs, uint32_t mtst, bool want, MtPre &q, int woff = 0) {
+__device__ __forceinline__ void mt_pre_load(const MtRes &rs, uint32_t mtst, bool want, MtPre &q) {
     int idx, pg, cur;
     mt_unpack(mtst, idx, pg, cur);
     const uint32_t cb = cur ? kMtB : 0u;
     u32x4 wv[WIN / 4];
 #pragma unroll
-    for (int i = 0; i < WIN / 4; ++i) wv[i] = mt_ld16(rs, want, cb + idx + woff + 4 * i);
+    for (int i = 0; i < WIN / 4; ++i) wv[i] = mt_ld16(rs, want, cb + idx + 4 * i);
 #pragma unroll
     for (int i = 0; i < WIN / 4; ++i)
         q.w[4 * i] = wv[i].x, q.w[4 * i + 1] = wv[i].y, q.w[4 * i + 2] = wv[i].z, q.w[4 * i + 3] = wv[i].w;
@@ -474,17 +474,10 @@ __device__ __attribute__((noinline)) void mt_finish(uint32_t *g, uint32_t *S, in
 // continue in the loop, switching generations at index 624.
 // COUNT: also count the drawn shape in cnt (a spawn's _new_piece :199; not
 // for a preview, which is counted when it spawns).
-// CACHED: lanes with `cv` first try the 4 cached words c4 (positions
-// idx..idx+3, no load to wait for); the window then sits at idx + woff
-// (woff = 4 for those lanes) and is waited for only if some lane needs it.
-// *fastpos: the position after the draw (before a generation switch) when the
-// prefetched words settled it, else -1.
-template <int WIN, bool COUNT = true, bool CACHED = false>
+template <int WIN, bool COUNT = true>
 __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t &mtst,
                                           uint32_t *mt_wave, uint32_t *S, int lane,
-                                          const MtPre &pre, bool have_pre,
-                                          const uint32_t *c4 = nullptr, bool cv = false, int woff = 0,
-                                          int *fastpos = nullptr) {
+                                          const MtPre &pre, bool have_pre) {
     int32_t maxc = cnt[0], sumc = cnt[0];
 #pragma unroll
     for (int i = 1; i < 7; ++i) {
@@ -497,8 +490,7 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
     mt_unpack(mtst, idx, pg, cur);
     bool pending = need;
     uint32_t r = 0;
-    if constexpr (!CACHED) mt_win_consume<WIN>(pre);
-    int fpos = -1;
+    mt_win_consume<WIN>(pre);
     if (have_pre && pending) {
         // The prefetched words sit at positions idx.. of the current
         // generation and, past 623, of the next one (cur[624..639] is
@@ -525,15 +517,9 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
                 pos = p0 + NW < lim ? p0 + NW : lim;
             }
         };
-        using I4 = std::integral_constant<int, 4>;
         using I8 = std::integral_constant<int, 8>;
-        if constexpr (CACHED) {
-            if (cv) pass(c4, idx, I4{});
-        }
-        const int b = idx + woff;
-        if (!CACHED || __ballot(pending && pos == b)) {
-            if (pending && pos == b) pass(pre.w, b, I8{});
-        }
+        const int b = idx;
+        if (pending) pass(pre.w, b, I8{});
         // 8 rejections in a row (p <= 2^-8 per draw, a few lanes per step):
         // the next 8 words are already here, no dependent load
         if constexpr (WIN > 8) {
@@ -541,7 +527,6 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
                 if (pending && pos == b + 8) pass(pre.w + 8, b + 8, I8{});
             }
         }
-        if (!pending) fpos = pos;
         if (pos > kMtN) {  // the draw ran into the (complete) next generation
             cur ^= 1;
             pos -= kMtN;
@@ -589,7 +574,6 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
         } while (__ballot(pending));
     }
     if (need) mtst = mt_keep(mtst, mt_pack(idx, pg, cur));
-    if (fastpos) *fastpos = fpos;
     if (!need) return 0;
     int32_t rr = (int32_t)r + 1;
     int pick = 6;
@@ -653,9 +637,6 @@ struct StepLds {
     // before the other has read step t's)
     uint32_t lockm[2][2], drawm[2];
     uint32_t pick1[kWave];
-    // st_step draw wave: per lane [cache 4 | window 16] words, to pick the
-    // next cache (4 words at the new position) by a dynamic offset
-    uint32_t cw[KSTEPS == 1 ? kWave * 20 : 4] __attribute__((aligned(16)));
     uint32_t mtw[2][KSTEPS == 1 ? 1 : kWave];  // rollouts: the draw wave's MT word after step t
     uint32_t f1, f2;  // = t + 1 once step t's draw mask / first picks are written
 };
@@ -781,7 +762,6 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         if (mine_q(q))
             sv[q] = *reinterpret_cast<const uint4 *>(ssrc + (size_t)(4 * q) * sd +
                                                      (4 * q + 4 <= kHotRows ? loff : clamp_off(q, kHotRows)));
-    [[maybe_unused]] uint4 c4v = make_uint4(0u, 0u, 0u, 0u);
     const int K = KSTEPS ? KSTEPS : p.k;
     // two-wave st_step: the logic wave also builds the next-generation block
     // (the draw wave's chain is the longer one).  (Measured and dropped: the
@@ -866,9 +846,6 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         if (ROLE == kRoleL && lane == 0) sm.f1 = 0u;
         if (ROLE == kRoleD && lane == 0) sm.f2 = 0u;
         wg_barrier();  // B0: the staged state is complete
-        // the draw wave's cache words: loaded now (not in the prologue's
-        // burst), they arrive while it waits for the lock ballot at B1
-        if constexpr (KSTEPS == 1 && ROLE == kRoleD) c4v = *reinterpret_cast<const uint4 *>(p.mtc + 4 * e);
     } else {
         wave_sync();
     }
@@ -981,17 +958,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
     const bool want_pre = locknow && !(kAblate & 2u);
     constexpr int kWin = STEP2 ? 8 : 16;
     MtPre pre;
-    // st_step: lanes whose draw-window cache is valid take their first 4 words
-    // from it (loaded after B0) and load the window 4 words further on
-    [[maybe_unused]] const bool cv = STEP2 && cache_ok(mt0);
-    [[maybe_unused]] const int woff = cv ? 4 : 0;
-    if constexpr (DO_D) {
-        // the cache words to the lane's LDS row before the window loads are
-        // issued: their wait is here, not after the draw's branchy first-draw
-        // path, where it would become a vmcnt(0) on the window
-        if constexpr (STEP2) *reinterpret_cast<uint4 *>(&sm.cw[lane * 12]) = c4v;
-        mt_pre_load<kWin>(mrs, mtst, want_pre, pre, woff);
-    }
+    if constexpr (DO_D) mt_pre_load<kWin>(mrs, mtst, want_pre, pre);
 
     // ---------------- logic: lock path (tetris_env.py:263-299) ----------------
     bool died = false, spawn = false;
@@ -1192,15 +1159,13 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
 #pragma unroll
         for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)ss(ST_STAT_COUNT0 + i);  // used by drawing lanes only
         if constexpr (STAMP) {  // diagnostic split of the draw: MT-word wait | compute
-            if constexpr (!STEP2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (st_step: the cache pass does not wait)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             ST_STAMP(9);
         }
         [[maybe_unused]] const uint32_t mt_before = mtst;
         uint32_t mt_new = mtst;
-        [[maybe_unused]] bool cvn = false;
-        [[maybe_unused]] uint4 n4 = make_uint4(0u, 0u, 0u, 0u);
         if (!(kAblate & 2u)) {
-            if constexpr (!STEP2) mt_win_consume<kWin>(pre);
+            mt_win_consume<kWin>(pre);
             const bool need1 = dr_spec && !pv_ok(mt0);
             if (__ballot(need1)) {  // rare: after st_seed / st_mt_sync / a host-written state
                 const int pk = draw_shape<kWin, false>(need1, cnt, mtst, p.mt + e0 * kMtPitch, sm.S, lane, pre, false);
@@ -1213,29 +1178,9 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
 #pragma unroll
             for (int i = 0; i < 7; ++i) cnt[i] += (dr_spec && i == sid);  // _new_piece :199
             const uint32_t m0 = mtst;
-            int fpos = -1;
-            const uint32_t c4a[4] = {c4v.x, c4v.y, c4v.z, c4v.w};
-            const int npv = draw_shape<kWin, false, STEP2>(dr_spec, cnt, mtst, p.mt + e0 * kMtPitch, sm.S, lane,
-                                                            pre, want_pre && pv_ok(mt0), c4a, cv, woff, &fpos);
-            if constexpr (STEP2) {
-                // the next cache: the 4 words at the new position, picked from
-                // [cache | window] (positions i0.. of the draw's start) through
-                // a per-lane LDS row; valid only if the fast passes settled the
-                // draw and the 4 words lie inside the window and below lim
-                uint32_t *row = &sm.cw[lane * 12];  // row[0..3] = the cache (stored before the draw)
-#pragma unroll
-                for (int q = 0; q < kWin / 4; ++q)
-                    *reinterpret_cast<uint4 *>(row + woff + 4 * q) =
-                        make_uint4(pre.w[4 * q], pre.w[4 * q + 1], pre.w[4 * q + 2], pre.w[4 * q + 3]);
-                int i0, pg0, c0;
-                mt_unpack(m0, i0, pg0, c0);
-                const int lim0 = pg0 == kMtN ? kMtN + kWin : kMtN;
-                const int off = fpos - i0;
-                cvn = fpos >= 0 && off + 3 <= woff + kWin - 1 && fpos + 3 < lim0;
-                const int o = cvn ? off : 0;
-                n4 = make_uint4(row[o], row[o + 1], row[o + 2], row[o + 3]);
-            }
-            mt_new = pv_pack(mtst, npv, mt_consumed(m0, mtst), cvn);
+            const int npv = draw_shape<kWin, false>(dr_spec, cnt, mtst, p.mt + e0 * kMtPitch, sm.S, lane, pre,
+                                                    want_pre && pv_ok(mt0));
+            mt_new = pv_pack(mtst, npv, mt_consumed(m0, mtst));
         } else if constexpr (TWO) {
             sm.pick1[lane] = (uint32_t)sid;
             if (lane == 0) lds_flag_set(&sm.f2, (uint32_t)t + 1u);
@@ -1261,10 +1206,6 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
             }
         }
         [[maybe_unused]] uint32_t sdd = 0;
-        if constexpr (STEP2) {  // the next draw-window cache (lanes that drew and have one)
-            const auto rc = buf_rsrc(p.mtc, (uint32_t)sd * 16u);
-            buf_store16<kNT>(rc, dr && cvn ? (uint32_t)e * 16u : kOff, n4);
-        }
         // (a lane that locks but does not draw -- a death without auto-reset
         // -- keeps its old MT word: its speculative draw is dropped)
         uint32_t mt_out = dr ? mt_new : mt0;
