@@ -8,7 +8,9 @@ TetrisEnv     -- the reference's single-env class (tetris_env.py:338-467):
                  exactly as the reference's do (tetris_env.py:187): the global
                  MT19937 state is uploaded before and read back after every
                  call, so a program that seeds `random` gets the reference's
-                 games bit-for-bit.
+                 games bit-for-bit.  Its GPU work is issued on the stream
+                 that was current when it was constructed, with one
+                 synchronize per call.
 TetrisVecEnv  -- the batched surface: N envs, torch tensors on the GPU,
                  per-env CPython MT19937 streams random.seed(seed + e).
 Both run every game rule in the HIP kernels (engine.TetrisBatch); there is no
@@ -39,6 +41,25 @@ def _obs_space(obs_type, width, height, extend_dims):
     else:
         return None
     return spaces.Box(0, 1, shape=shape, dtype=np.float32)
+
+
+def _stream_sync(sp: ctypes.c_void_p, device):
+    """A synchronize of stream `sp`: hipStreamSynchronize through ctypes, or
+    torch's where the HIP runtime library cannot be opened by name."""
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        fn = hip.hipStreamSynchronize
+        fn.argtypes = [ctypes.c_void_p]
+        fn.restype = ctypes.c_int
+
+        def sync():
+            rc = fn(sp)
+            if rc != 0:
+                raise RuntimeError(f"hipStreamSynchronize failed ({rc})")
+        return sync
+    except (OSError, AttributeError):
+        stream = torch.cuda.current_stream(device)
+        return stream.synchronize
 
 
 def _mapped(t: torch.Tensor):
@@ -116,6 +137,14 @@ class TetrisEnv:
         # when the runtime maps them for the device (else: device buffer + copy)
         self._rec_dst = _mapped(self._h_rec)
         self._img_dst = _mapped(self._h_img) if obs_type in ("grayscale", "rgb") else None
+        # per-step constants: output pointers, the stream current at
+        # construction (the env issues all its work there), a direct
+        # hipStreamSynchronize (torch's costs ~3 us more per call)
+        self._po, self._pr, self._pd = (ctypes.c_void_p(t.data_ptr())
+                                        for t in (self.engine.obs, self.engine.reward, self.engine.done))
+        self._pz = ctypes.c_void_p(self._zeros.data_ptr())
+        self._sp = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        self._sync = _stream_sync(self._sp, dev)
 
     # ------------------------------------------------------------- RNG mirror
     def seed(self, seed=None):
@@ -128,7 +157,7 @@ class TetrisEnv:
         return [seed]
 
     def _stream(self):
-        return ctypes.c_void_p(torch.cuda.current_stream(self.engine.device).cuda_stream)
+        return self._sp
 
     def _push_rng(self):
         if self._rng_mode != "global":
@@ -172,13 +201,13 @@ class TetrisEnv:
                 C.check(L.st_grayscale(ctx, src, 84, self._ch, 0, ctypes.c_void_p(self._d_img.data_ptr()), s))
                 C.check(L.st_copy(ctypes.c_void_p(self._h_img.data_ptr()), ctypes.c_void_p(self._d_img.data_ptr()),
                                   self._d_img.numel() * 4, s))
-        torch.cuda.current_stream(eng.device).synchronize()
+        self._sync()
         rec = self._h_rec_np
         W = self.width
         words = rec[:W].view(np.uint32).copy()
-        st = rec[W + 2: W + 2 + C.NSTAT].astype(np.int64)
+        st = rec[W + 2: W + 2 + C.NSTAT].tolist()  # Python ints (the reference's counters are ints)
         if self._rng_mode == "global":
-            idx = int(st[C.STAT["mt_index"]])
+            idx = st[C.STAT["mt_index"]]
             if prev_idx is None or idx != prev_idx or self._rng_sync_state is None:
                 mt = rec[W + 2 + C.NSTAT:].view(np.uint32)
                 old = random.getstate()
@@ -216,7 +245,7 @@ class TetrisEnv:
         if done:
             return int(r)
         c0 = C.STAT["count0"]
-        locked = int(st[c0:c0 + 7].sum()) > int(prev[c0:c0 + 7].sum())
+        locked = sum(st[c0:c0 + 7]) > sum(prev[c0:c0 + 7])
         if not locked:
             return int(r)
         if self._scoring["advanced_clears"]:
@@ -237,9 +266,8 @@ class TetrisEnv:
         prev = self._stats
         self._push_rng()
         eng = self.engine
-        po, pr, pd = (ctypes.c_void_p(t.data_ptr()) for t in (eng.obs, eng.reward, eng.done))
-        C.check(eng._L.st_step(eng._ctx, self._p_acts[int(action)], po, pr, pd, self._stream()))
-        words, r, d, st, img = self._readback(po, pr, pd, int(prev[C.STAT["mt_index"]]))
+        C.check(eng._L.st_step(eng._ctx, self._p_acts[int(action)], self._po, self._pr, self._pd, self._sp))
+        words, r, d, st, img = self._readback(self._po, self._pr, self._pd, prev[C.STAT["mt_index"]])
         self._stats = st
         return self._observation(words, img), self._typed_reward(r, d, prev, st), d, self._get_info(st)
 
@@ -247,9 +275,9 @@ class TetrisEnv:
         """TetrisEnv.reset (tetris_env.py:405-411): clear(); obs is the empty
         board (clear() returns the board before the new piece is drawn)."""
         self._push_rng()
-        self.engine.reset()
+        C.check(self.engine._L.st_reset(self.engine._ctx, None, self._sp))  # clear() on the env's stream
         self._started = True
-        words, _, _, st, img = self._readback(ctypes.c_void_p(self._zeros.data_ptr()), None, None)
+        words, _, _, st, img = self._readback(self._pz, None, None)
         self._stats = st
         obs = self._observation(words, img)
         return (obs, self._get_info(st)) if return_info else obs
@@ -257,6 +285,7 @@ class TetrisEnv:
     def render(self, mode="human"):
         """render('rgb_array'): 160x160x3 uint8 frame (tetris_env.py:458-462)."""
         if mode == "rgb_array":
+            self._sync()  # the env's own stream first (its steps), then the current one
             packed = self.engine.render_packed()
             img = self.engine.grayscale(packed, 160, 3, as_u8=True)[0]
             return img.cpu().numpy()
