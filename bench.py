@@ -477,7 +477,7 @@ def main():
         w.close()
         variants.update(image_variants(head, C, timed, roofline, dev, s, sp, W, WU, K))
         if world == 1:
-            variants["single_env"] = single_env_variant(min(K, 2000))
+            variants["single_env"] = single_env_variant(2000)
         if not args.no_clear_heavy and not f32:
             variants["step_clear_heavy"] = clear_heavy(head, cfg_kw, C, ShardedTetris, timed, roofline,
                                                        kname_of, dev, s, sp, rank, world, W, H, K, WU,
