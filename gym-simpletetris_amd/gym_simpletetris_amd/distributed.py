@@ -10,7 +10,10 @@ The one exchange the north star names -- delivering every shard's packed
 obs / reward / done to rank 0 -- is `gather_outputs`: one torch.distributed
 gather (RCCL over xGMI with the 'nccl' backend; gloo on CPU in the tests) of a
 single contiguous int32 buffer per rank, laid out [W + 2][n_local]:
-rows 0..W-1 packed obs words, row W reward, row W+1 done bytes.
+rows 0..W-1 packed obs words, row W reward, row W+1 done bytes.  Collective
+gathers need one size on every rank, so when n_global % world != 0 the short
+ranks pad their buffer to the longest shard (`shard_cap`) for the transfer and
+`assemble` drops the padding columns again.
 """
 from __future__ import annotations
 
@@ -31,6 +34,11 @@ def shard_range(n_global: int, world: int, rank: int) -> Tuple[int, int]:
     return offset, count
 
 
+def shard_cap(n_global: int, world: int) -> int:
+    """Columns of the largest shard (rank 0's): the gather's common width."""
+    return -(-n_global // world)
+
+
 def output_buffer(width: int, n_local: int, device) -> torch.Tensor:
     """The per-rank packed output buffer [W + 2][n_local] int32."""
     return torch.zeros((width + 2, n_local), dtype=torch.int32, device=device)
@@ -43,21 +51,37 @@ def buffer_views(buf: torch.Tensor, width: int):
     return buf[:width], buf[width], done
 
 
-def gather_outputs(buf: torch.Tensor, group=None, dst: int = 0) -> Optional[List[torch.Tensor]]:
-    """Gather every rank's packed buffer to `dst` (equal shard sizes)."""
+def gather_outputs(buf: torch.Tensor, group=None, dst: int = 0,
+                   n_cap: Optional[int] = None) -> Optional[List[torch.Tensor]]:
+    """Gather every rank's packed buffer to `dst`.  `n_cap` (default: this
+    buffer's width) is the common column count; a shorter buffer is sent
+    zero-padded to it, so ragged shards (shard_range with n_global % world
+    != 0) gather correctly.  Returns the [W + 2][n_cap] buffers on `dst`."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    bufs = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
-    dist.gather(buf, gather_list=bufs, dst=dst, group=group)
+    rows, n = buf.shape
+    n_cap = n if n_cap is None else n_cap
+    if n > n_cap:
+        raise ValueError(f"shard of {n} envs exceeds the gather width {n_cap}")
+    send = buf
+    if n < n_cap:
+        send = buf.new_zeros((rows, n_cap))
+        send[:, :n] = buf
+    bufs = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
+    dist.gather(send, gather_list=bufs, dst=dst, group=group)
     return bufs
 
 
-def assemble(bufs: List[torch.Tensor], width: int):
+def assemble(bufs: List[torch.Tensor], width: int, counts: Optional[List[int]] = None):
     """Rank-0 side: concatenate gathered buffers into global (obs [W][N],
-    reward [N], done [N]) in global env order."""
-    obs = torch.cat([b[:width] for b in bufs], dim=1)
-    reward = torch.cat([b[width] for b in bufs])
-    done = torch.cat([buffer_views(b, width)[2] for b in bufs])
+    reward [N], done [N]) in global env order; `counts[r]` = rank r's real
+    envs (shard_range), default every column of every buffer."""
+    counts = [b.shape[1] for b in bufs] if counts is None else counts
+    if len(counts) != len(bufs):
+        raise ValueError(f"{len(counts)} counts for {len(bufs)} buffers")
+    obs = torch.cat([b[:width, :c] for b, c in zip(bufs, counts)], dim=1)
+    reward = torch.cat([b[width, :c] for b, c in zip(bufs, counts)])
+    done = torch.cat([buffer_views(b, width)[2][:c] for b, c in zip(bufs, counts)])
     return obs, reward, done
 
 
@@ -70,6 +94,8 @@ class ShardedTetris:
         self.rank = dist.get_rank() if rank is None else rank
         self.world = dist.get_world_size() if world is None else world
         self.offset, self.n = shard_range(n_global, self.world, self.rank)
+        self.n_cap = shard_cap(n_global, self.world)
+        self.counts = [shard_range(n_global, self.world, r)[1] for r in range(self.world)]
         self.engine = TetrisBatch(self.n, device=device,
                                   seeds=[seed + self.offset + e for e in range(self.n)],
                                   **engine_kwargs)
@@ -86,5 +112,10 @@ class ShardedTetris:
 
     def gather(self, dst: int = 0, cpu: bool = False):
         """RCCL gather of the packed outputs to `dst` (cpu=True: via host
-        memory, for the gloo backend in tests)."""
-        return gather_outputs(self.buf.cpu() if cpu else self.buf, dst=dst)
+        memory, for the gloo backend in tests); padded to `n_cap` columns,
+        pass the result to `assemble` for the global (obs, reward, done)."""
+        return gather_outputs(self.buf.cpu() if cpu else self.buf, dst=dst, n_cap=self.n_cap)
+
+    def assemble(self, bufs: List[torch.Tensor]):
+        """Global (obs [W][N], reward [N], done [N]) from gather()'s result."""
+        return assemble(bufs, self.engine.width, self.counts)

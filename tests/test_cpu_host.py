@@ -98,14 +98,14 @@ def test_grayscale_closed_form_matches_reference_images():
             assert np.array_equal(img, d[key][i]), (i, size)
 
 
-def _gather_worker(rank, world, port, q):
+def _gather_worker(rank, world, port, q, n_global):
     import torch.distributed as dist
     from gym_simpletetris_amd.distributed import (assemble, buffer_views, gather_outputs,
-                                                  output_buffer, shard_range)
+                                                  output_buffer, shard_cap, shard_range)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    W, n_global = 10, 64
+    W = 10
     off, n = shard_range(n_global, world, rank)
     buf = output_buffer(W, n, "cpu")
     obs, rew, done = buffer_views(buf, W)
@@ -113,9 +113,9 @@ def _gather_worker(rank, world, port, q):
     obs[:] = g[None, :] * 16 + torch.arange(W, dtype=torch.int32)[:, None]
     rew[:] = -g
     done[:] = (g % 3 == 0).to(torch.uint8)
-    bufs = gather_outputs(buf)
+    bufs = gather_outputs(buf, n_cap=shard_cap(n_global, world))
     if rank == 0:
-        o, r, d = assemble(bufs, W)
+        o, r, d = assemble(bufs, W, [shard_range(n_global, world, i)[1] for i in range(world)])
         ok = (torch.equal(r, -torch.arange(n_global, dtype=torch.int32))
               and torch.equal(d, (torch.arange(n_global) % 3 == 0).to(torch.uint8))
               and torch.equal(o[3], torch.arange(n_global, dtype=torch.int32) * 16 + 3))
@@ -123,7 +123,9 @@ def _gather_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_gather_packing_gloo_world2():
+@pytest.mark.parametrize("world,n_global", [(2, 64), (2, 67), (3, 67)])
+def test_gather_packing_gloo(world, n_global):
+    """Even and ragged shards (short ranks send a padded buffer)."""
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
@@ -132,7 +134,8 @@ def test_gather_packing_gloo_world2():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q, n_global))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -1,9 +1,10 @@
 """The N > 1 path on one GPU box (VERDICT r1 "next" #2).
 
 1. Two rank processes (torch.distributed, gloo: both ranks share cuda:0 on a
-   one-GPU box) each step their ShardedTetris shard of a 2n-env batch and
+   one-GPU box) each step their ShardedTetris shard of a (2n + 1)-env batch
+   (ragged: rank 0 holds one env more, so rank 1 sends a padded buffer) and
    gather the packed obs / reward / done to rank 0 every step; rank 0's
-   assembled global outputs must equal one process stepping all 2n envs
+   assembled global outputs must equal one process stepping all 2n + 1 envs
    (the split is by global env index: seeds and actions keyed by it).
 2. `python bench.py --gpus 2` run directly (no torch.distributed.run): it
    starts its own two ranks and prints one JSON line with the gather variant.
@@ -29,7 +30,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 sys.path[:0] = [{root!r}, os.path.join({root!r}, "gym-simpletetris_amd")]
-from gym_simpletetris_amd.distributed import ShardedTetris, assemble
+from gym_simpletetris_amd.distributed import ShardedTetris
 dist.init_process_group("gloo")
 rank, world = dist.get_rank(), dist.get_world_size()
 sh = ShardedTetris({n_global}, seed={seed}, device=torch.device("cuda", 0), autoreset="same_step",
@@ -42,7 +43,7 @@ for t in range({steps}):
     torch.cuda.synchronize()
     bufs = sh.gather(cpu=True)
     if rank == 0:
-        o, r, d = assemble(bufs, sh.engine.width)
+        o, r, d = sh.assemble(bufs)
         obs.append(o.numpy()); rew.append(r.numpy()); done.append(d.numpy())
 if rank == 0:
     np.savez({out!r}, obs=np.stack(obs), rew=np.stack(rew), done=np.stack(done))
@@ -60,7 +61,7 @@ def _port():
 def test_two_ranks_gather_equals_one_batch(tmp_path):
     out = str(tmp_path / "gathered.npz")
     script = tmp_path / "worker.py"
-    script.write_text(WORKER.format(root=ROOT, n_global=2 * N_LOCAL, seed=SEED, steps=T, aseed=ASEED,
+    script.write_text(WORKER.format(root=ROOT, n_global=2 * N_LOCAL + 1, seed=SEED, steps=T, aseed=ASEED,
                                     out=out))
     port = _port()
     procs = []
@@ -73,7 +74,7 @@ def test_two_ranks_gather_equals_one_batch(tmp_path):
     got = np.load(out)
 
     import gym_simpletetris_amd as G
-    n = 2 * N_LOCAL
+    n = 2 * N_LOCAL + 1
     b = G.TetrisBatch(n, autoreset="same_step", seeds=[SEED + e for e in range(n)],
                       penalise_holes_increase=True)
     b.reset()
