@@ -206,8 +206,10 @@ def main():
     ap.add_argument("--n-envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c3")
     ap.add_argument("--obs", choices=("packed", "f32"), default="packed")
-    ap.add_argument("--launch", choices=("graph", "eager"), default="graph",
-                    help="timed steps as one hipGraph of K st_step launches, or K eager launches")
+    ap.add_argument("--launch", choices=("graph", "eager"), default="eager",
+                    help="timed steps as K eager st_step launches, or one hipGraph of them "
+                         "(measured: graph replay 2.5%% slower at K=4000, noisier at K=20; "
+                         "profiles/r02_launch_ab.jsonl)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--rollout-chunk", type=int, default=100, help="steps per st_rollout launch")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
