@@ -117,8 +117,9 @@ def _compare(t0, got_r, got_d, got_o, ref):
     assert bad.size == 0, f"obs mismatch at (step, env) {bad[:4] + [t0, 0]}"
 
 
-@pytest.mark.parametrize("config", sorted(CONFIGS))
-def test_bench_workload_st_step_graph(config):
+@pytest.mark.parametrize("config,launch", [("c3", "eager"), ("c3", "graph"), ("c4", "eager")])
+def test_bench_workload_st_step(config, launch):
+    """bench.py's headline region (eager: the default; graph: `--launch graph`)."""
     import gym_simpletetris_amd as G
     from gym_simpletetris_amd import _lib as C
     dev = torch.device("cuda", 0)
@@ -145,14 +146,20 @@ def test_bench_workload_st_step_graph(config):
         for t in range(WU):  # bench warm-up: eager launches
             launch(t)
     torch.cuda.synchronize(dev)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=s):  # bench timed region: one graph of K launches
-        for t in range(WU, T):
-            launch(t)
-    with torch.cuda.stream(s):
-        g.replay()
-    torch.cuda.synchronize(dev)
-    del g
+    if launch == "graph":
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):  # bench --launch graph: one graph of K launches
+            for t in range(WU, T):
+                launch(t)
+        with torch.cuda.stream(s):
+            g.replay()
+        torch.cuda.synchronize(dev)
+        del g
+    else:
+        with torch.cuda.stream(s):  # bench default: K eager launches
+            for t in range(WU, T):
+                launch(t)
+        torch.cuda.synchronize(dev)
     orc = ParallelOracle(N, kw)
     try:
         CH = 100
