@@ -124,6 +124,23 @@ def load_pmc(kname: str, sha: str):
     return None, f"no PMC pass of these kernel sources (sha {sha}) under profiles/"
 
 
+def load_trace(kname: str, sha: str):
+    """rocprofv3 kernel-trace duration stats of `kname` (`name@grid`, the
+    longest run of launches) from a committed profiles/*_trace.json
+    (tools/trace_summary.py --json) of the same kernel sources; None if none."""
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_trace.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except Exception:  # noqa: BLE001
+            continue
+        if d.get("kernel_source_sha") != sha:
+            continue
+        v = d.get("kernels", {}).get(kname)
+        if v is not None:
+            return dict(v, source=os.path.basename(f))
+    return None
+
+
 # ----------------------------------------------------------------------------- CPU baseline
 def cpu_model() -> str:
     try:
@@ -326,6 +343,11 @@ def main():
              "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
              "kernel_us": kern_us, "bytes_per_env_step": bpe, "bytes_per_launch": bpl,
              "traffic_source": src, "kernel_source_sha": sha}
+        tr = load_trace(f"{kname}@{grid}", sha) if grid is not None else None
+        if tr is not None:  # the committed rocprofv3 trace of the same sources
+            r["rocprof"] = {"mean_us": tr["mean_us"], "median_us": tr["median_us"],
+                            "launches": tr["launches"], "source": f"{tr['source']} ({tr['trace']})",
+                            "frac_at_traced_mean": bpl / (tr["mean_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS}
         if extra:
             r.update(extra)
         return r
@@ -552,8 +574,9 @@ def image_variants(head, C, timed, roofline, dev, s, sp, W, WU, K):
         kern_us = ev * 1e3 / KG
         bpe = 4 * W + 84 * 84 * ch * 4
         r = {"kernel_only": True, "launches": KG, "kernel_us": kern_us,
-             "roofline": roofline(kern_us, bpe, n, "k_grayscale<float, 1>",
-                                  {"bytes_formula": f"read packed obs 4W + write 84*84*{ch}*4 per env"})}
+             "roofline": roofline(kern_us, bpe, n, f"k_grayscale<float, {ch}>",
+                                  {"bytes_formula": f"read packed obs 4W + write 84*84*{ch}*4 per env"},
+                                  grid=(n + 15) // 16 * 256)}  # launch_grayscale: 16 envs per 256-thread block
         # whole steps with this obs_type: st_step + the image per step
         KS = max(1, min(K, 100))
 

@@ -168,6 +168,13 @@ def test_bench_roofline_bytes_and_pmc_tie():
     got, why = bench.load_pmc(kname, "0" * 16)
     assert got is None and "no PMC pass" in why
     assert len(bench.kernel_source_sha()) == 16
+    # the rocprofv3 trace stats come the same way, from a trace of the same sources
+    tj = json.load(open(os.path.join(ROOT, "profiles", "r02_trace.json")))
+    tr = bench.load_trace(kname, tj["kernel_source_sha"])
+    assert tr["launches"] == tj["kernels"][kname]["launches"] and tr["source"] == "r02_trace.json"
+    assert bench.load_trace(kname, "0" * 16) is None
+    # the committed profiles describe the committed kernel sources
+    assert d["kernel_source_sha"] == tj["kernel_source_sha"] == bench.kernel_source_sha()
 
 
 def test_bench_cpu_baseline_all_cores():

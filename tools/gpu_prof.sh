@@ -2,7 +2,8 @@
 # Profiling pass for one round's numbers (TAG=r02 bash tools/gpu_prof.sh):
 #  1. rocprofv3 --kernel-trace --stats of the default bench command (all
 #     variants) and of the headline alone (--no-extras: clean per-kernel stats),
-#     plus tools/trace_summary.py per-run splits of both traces
+#     plus tools/trace_summary.py per-run splits of both traces and their
+#     per-kernel@grid JSON -> gpurun_out/${TAG}_trace.json (copy to profiles/)
 #  2. PMC: FETCH_SIZE and WRITE_SIZE in SEPARATE passes (TCC slot limits) over
 #     eager launches of every variant, plus the same two passes over
 #     tools/pmc_calib (known byte counts) -> tools/pmc_summary.py ->
@@ -24,5 +25,6 @@ run rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$TAG" -o fu
  && run rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$O/pmc_cal_write_$TAG" -o cal -- "$R/tools/pmc_calib" >> "$O/prof_$TAG.err" 2>&1 \
  && (cd "$R" && python3 tools/pmc_summary.py "$TAG" "$O/pmc_fetch_$TAG" "$O/pmc_write_$TAG" "$O/pmc_cal_fetch_$TAG" "$O/pmc_cal_write_$TAG" > "$O/pmc_summary_$TAG.json" && cp "profiles/${TAG}_pmc.json" "$O/") \
  && (cd "$R" && python3 tools/trace_summary.py "$O/prof_$TAG/full_kernel_trace.csv" > "$O/trace_summary_$TAG.txt" \
-     && python3 tools/trace_summary.py "$O/prof_$TAG/head_kernel_trace.csv" > "$O/trace_summary_head_$TAG.txt") \
+     && python3 tools/trace_summary.py "$O/prof_$TAG/head_kernel_trace.csv" > "$O/trace_summary_head_$TAG.txt" \
+     && python3 tools/trace_summary.py --json "$TAG" "$O/prof_$TAG/head_kernel_trace.csv" "$O/prof_$TAG/full_kernel_trace.csv" > "$O/${TAG}_trace.json") \
  && echo "prof ok"

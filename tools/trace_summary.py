@@ -1,6 +1,10 @@
 """Per-kernel duration distribution from a rocprofv3 kernel trace (csv).
 
 usage: python tools/trace_summary.py <..._kernel_trace.csv> [min_run]
+       python tools/trace_summary.py --json TAG <..._kernel_trace.csv>...
+         -> JSON on stdout: per engine kernel@grid, the longest run's traced
+            duration stats, with bench.kernel_source_sha() of the sources
+            (profiles/<TAG>_trace.json, read by bench.py's roofline)
 
 bench.py launches the same kernel in several workloads (the headline's
 warm-up and timed graph, the C2 batch with a smaller grid, the clear-heavy
@@ -19,9 +23,7 @@ def short(name):
     return name.replace("st::(anonymous namespace)::", "").replace("void ", "").split("(")[0]
 
 
-def main():
-    path = sys.argv[1]
-    min_run = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+def split_runs(path):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     runs = []  # [key, [durations]]
@@ -33,6 +35,37 @@ def main():
             runs[-1][1].append(d)
         else:
             runs.append([key, [d]])
+    return runs
+
+
+def stats(v):
+    s = sorted(v)
+    q = lambda f: s[min(len(s) - 1, int(f * len(s)))] / 1e3  # noqa: E731
+    return {"launches": len(v), "mean_us": statistics.mean(v) / 1e3,
+            "median_us": statistics.median(v) / 1e3, "p10_us": q(0.1), "p90_us": q(0.9)}
+
+
+def to_json(tag, paths):
+    import json
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    longest = {}
+    for path in paths:  # earlier files win ties
+        for key, v in split_runs(path):
+            k = f"{key[0]}@{key[1]}"
+            if key[0].startswith("k_") and len(v) > longest.get(k, {}).get("launches", 0):
+                longest[k] = dict(stats(v), trace=os.path.basename(path))
+    print(json.dumps({"tag": tag, "kernel_source_sha": bench.kernel_source_sha(),
+                      "kernels": longest}, indent=1))
+
+
+def main():
+    if sys.argv[1] == "--json":
+        return to_json(sys.argv[2], sys.argv[3:])
+    path = sys.argv[1]
+    min_run = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+    runs = split_runs(path)
     print(f"{'run':>3s} {'kernel':42s} {'grid':>8s} {'calls':>6s} {'mean_us':>8s} {'median':>8s} "
           f"{'p10':>8s} {'p90':>8s}")
     for i, (key, v) in enumerate(runs):
