@@ -32,6 +32,15 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[ctypes.c_void_p]:
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+def _from_dlpack(x):
+    """A foreign device array (any DLPack producer: __dlpack__ /
+    __dlpack_device__, e.g. a learner's action buffer) as a torch tensor over
+    the same memory -- no copy; torch tensors and numpy arrays pass through."""
+    if isinstance(x, (torch.Tensor, np.ndarray)) or not hasattr(x, "__dlpack__"):
+        return x
+    return torch.from_dlpack(x)
+
+
 class TetrisBatch:
     """Batched engine.  `autoreset`: 'none' (exact reference semantics; the
     caller resets done envs, like `if done: env.reset()`) or 'same_step'
@@ -128,6 +137,7 @@ class TetrisBatch:
         self._seeded = True
 
     def _as_dev_u8(self, x, name) -> torch.Tensor:
+        x = _from_dlpack(x)
         if isinstance(x, torch.Tensor):
             t = x.to(device=self.device, dtype=torch.uint8)
         else:
@@ -142,6 +152,7 @@ class TetrisBatch:
         7): the reference raises KeyError for an action outside
         value_action_map (tetris_env.py:152-160, :245)."""
         shape = tuple(lead) + (self.n,)
+        x = _from_dlpack(x)
         if isinstance(x, torch.Tensor):
             if x.dtype.is_floating_point or x.dtype == torch.bool or x.is_complex():
                 raise TypeError(f"actions must be integers, got {x.dtype}")
@@ -212,6 +223,7 @@ class TetrisBatch:
         [K, n, W, H] ('f32') or None ('none'); reward int32 [K, n]; done bool
         [K, n].  Identical to K calls of step().  `out` may supply the output
         tensors (keys 'obs', 'obs_f32', 'reward', 'done') to reuse buffers."""
+        actions = _from_dlpack(actions)
         if not isinstance(actions, torch.Tensor) or actions.dim() != 2 or actions.shape[1] != self.n \
                 or actions.shape[0] < 1:
             raise ValueError(f"actions must be a [K, {self.n}] integer tensor")

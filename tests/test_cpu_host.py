@@ -182,3 +182,23 @@ def test_bench_cpu_baseline_all_cores():
     cb = bench.cpu_baseline(0.2, "c4")
     assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0 and cb["single_core"] > 0
     assert cb["nproc"] >= 1 and cb["cpu_model"]
+
+
+def test_dlpack_producer_passes_through_without_copy():
+    from gym_simpletetris_amd.engine import _from_dlpack
+
+    class Foreign:
+        def __init__(self, t):
+            self.t = t
+
+        def __dlpack__(self, stream=None, **kw):
+            return self.t.__dlpack__()
+
+        def __dlpack_device__(self):
+            return self.t.__dlpack_device__()
+    t = torch.arange(7, dtype=torch.uint8)
+    u = _from_dlpack(Foreign(t))
+    assert isinstance(u, torch.Tensor) and u.data_ptr() == t.data_ptr() and torch.equal(u, t)
+    assert _from_dlpack(t) is t
+    a = np.arange(3)
+    assert _from_dlpack(a) is a
