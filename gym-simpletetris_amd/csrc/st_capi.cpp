@@ -253,17 +253,20 @@ int st_render(st_ctx *c, uint32_t *d_obs, st_stream stream) {
 }
 
 int st_export_env(st_ctx *c, int64_t env, const uint32_t *d_obs, const int32_t *d_reward,
-                  const uint8_t *d_done, uint32_t *d_out, st_stream stream) {
+                  const uint8_t *d_done, uint32_t parts, uint32_t *d_out, st_stream stream) {
     if (!c || !d_out) return fail(ST_EINVAL, "st_export_env: null argument");
     if (env < 0 || env >= c->n) return fail(ST_EINVAL, "st_export_env: env %lld of %lld", (long long)env,
                                             (long long)c->n);
+    if (parts & ~(ST_EXPORT_MT | ST_EXPORT_OBS_F32)) return fail(ST_EINVAL, "st_export_env: parts 0x%x", parts);
     if (!c->seeded) return fail(ST_ESTATE, "st_export_env before st_seed");
     DeviceGuard g(c->device);
-    ST_HIP(st::launch_export(params(c), env, d_obs, d_reward, d_done, d_out, (hipStream_t)stream));
+    ST_HIP(st::launch_export(params(c), env, d_obs, d_reward, d_done, parts, d_out, (hipStream_t)stream));
     return ST_OK;
 }
 
-int st_export_words(int32_t width) { return width + 2 + ST_NSTAT + st::kMtN; }
+int st_export_words(int32_t width, int32_t height) {
+    return width + 2 + ST_NSTAT + st::kMtN + width * height;
+}
 
 int st_grayscale(st_ctx *c, const uint32_t *d_obs, int32_t size, int32_t channels, int32_t as_u8,
                  void *d_out, st_stream stream) {

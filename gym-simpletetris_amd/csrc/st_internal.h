@@ -61,7 +61,7 @@ hipError_t launch_rollout(const KParams &p, hipStream_t s);
 hipError_t launch_obs_f32(const KParams &p, const uint32_t *obs, float *out, hipStream_t s);
 hipError_t launch_render(const KParams &p, hipStream_t s);
 hipError_t launch_export(const KParams &p, int64_t env, const uint32_t *obs, const int32_t *rew,
-                         const uint8_t *done, uint32_t *out, hipStream_t s);
+                         const uint8_t *done, uint32_t parts, uint32_t *out, hipStream_t s);
 hipError_t launch_mt_sync(const KParams &p, hipStream_t s);
 hipError_t launch_policy_greedy(const KParams &p, uint64_t seed, int64_t t, uint32_t explore,
                                 uint8_t *out, hipStream_t s);

@@ -1646,14 +1646,17 @@ __global__ __launch_bounds__(kWave) void k_render(KParams p) {
 // ---------------------------------------------------------------- export
 // st_export_env: one env's outputs and state as one record (the single-env
 // surface's per-step read-back in one transfer): obs words | reward | done |
-// stats rows | MT words.  The MT index row and words are CPython's form,
-// computed read-only the way k_mt_sync rewrites them (the preview's words
-// given back, the generation holding that position): the env keeps its
-// preview and next-generation progress.
+// stats rows | MT words (optional) | float32 obs (optional).  The MT index
+// row and words are CPython's form, computed read-only the way k_mt_sync
+// rewrites them (the preview's words given back, the generation holding that
+// position): the env keeps its preview and next-generation progress.  The
+// float32 obs saves the host the bit unpacking (the record is written
+// straight into mapped pinned memory).
 __global__ __launch_bounds__(256) void k_export(KParams p, int64_t env, const uint32_t *obs,
-                                               const int32_t *rew, const uint8_t *done, uint32_t *out) {
-    const int W = p.W;
-    const int words = W + 2 + ST_NSTAT + kMtN;
+                                               const int32_t *rew, const uint8_t *done, uint32_t parts,
+                                               uint32_t *out) {
+    const int W = p.W, H = p.H;
+    const int head = W + 2 + ST_NSTAT;
     const uint32_t r = (uint32_t)p.stats[(int64_t)ST_STAT_MT_INDEX * p.stride + env];
     int idx = (int)(r & 0x3FFu);
     uint32_t cur = (r >> 20) & 1u;
@@ -1666,16 +1669,26 @@ __global__ __launch_bounds__(256) void k_export(KParams p, int64_t env, const ui
             cur ^= 1u;
         }
     }
-    const uint32_t *g = p.mt + env * kMtPitch + (cur ? kMtB : 0u);
-    for (int i = threadIdx.x; i < words; i += blockDim.x) {
+    for (int i = threadIdx.x; i < head; i += blockDim.x) {
         uint32_t v;
         if (i < W) v = obs ? obs[(int64_t)i * p.n + env] : 0u;
         else if (i == W) v = rew ? (uint32_t)rew[env] : 0u;
         else if (i == W + 1) v = done ? (uint32_t)done[env] : 0u;
         else if (i == W + 2 + ST_STAT_MT_INDEX) v = (uint32_t)idx;
-        else if (i < W + 2 + ST_NSTAT) v = (uint32_t)p.stats[(int64_t)(i - W - 2) * p.stride + env];
-        else v = g[i - W - 2 - ST_NSTAT];
+        else v = (uint32_t)p.stats[(int64_t)(i - W - 2) * p.stride + env];
         out[i] = v;
+    }
+    if (parts & ST_EXPORT_MT) {
+        const uint32_t *g = p.mt + env * kMtPitch + (cur ? kMtB : 0u);
+        for (int i = threadIdx.x; i < kMtN; i += blockDim.x) out[head + i] = g[i];
+    }
+    if (parts & ST_EXPORT_OBS_F32) {
+        float *f = reinterpret_cast<float *>(out + head + kMtN);
+        for (int i = threadIdx.x; i < W * H; i += blockDim.x) {
+            const int x = i / H, y = i - x * H;
+            const uint32_t w = obs ? obs[(int64_t)x * p.n + env] : 0u;
+            f[i] = (float)((w >> y) & 1u);
+        }
     }
 }
 
@@ -2036,8 +2049,8 @@ hipError_t launch_gen_actions(uint8_t *out, int64_t n, int64_t t, uint64_t seed,
 }
 
 hipError_t launch_export(const KParams &p, int64_t env, const uint32_t *obs, const int32_t *rew,
-                         const uint8_t *done, uint32_t *out, hipStream_t s) {
-    hipLaunchKernelGGL(k_export, dim3(1), dim3(256), 0, s, p, env, obs, rew, done, out);
+                         const uint8_t *done, uint32_t parts, uint32_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_export, dim3(1), dim3(256), 0, s, p, env, obs, rew, done, parts, out);
     return hipGetLastError();
 }
 

@@ -34,6 +34,7 @@ STAT = dict(time=0, score=1, lines=2, holes=3, piece_height=4, deaths=5, count0=
             piece=14, ep_time=15, ep_score=16, ep_lines=17, ep_holes=18)
 NSTAT = 19
 MT_N = 624
+EXPORT_MT, EXPORT_OBS_F32 = 1, 2  # st_export_env parts
 
 EXPORTS = ("st_create", "st_destroy", "st_seed", "st_reset", "st_step", "st_step_f32", "st_rollout",
            "st_obs_to_f32", "st_render", "st_grayscale", "st_state", "st_copy", "st_mt_sync", "st_state_bytes", "st_save",
@@ -76,6 +77,7 @@ def load(path: str = LIB_PATH):
             "`make -C gym-simpletetris_amd/csrc` (the engine has no CPU fallback)")
     L = ctypes.CDLL(path)
     vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
+    u32 = ctypes.c_uint32
     sig = {
         "st_create": ([ctypes.POINTER(vp), ctypes.POINTER(Config), ctypes.c_int, i64], ctypes.c_int),
         "st_destroy": ([vp], ctypes.c_int),
@@ -93,8 +95,8 @@ def load(path: str = LIB_PATH):
         "st_state_bytes": ([vp], i64),
         "st_save": ([vp, vp, i64], ctypes.c_int),
         "st_load": ([vp, vp, i64], ctypes.c_int),
-        "st_export_env": ([vp, i64, vp, vp, vp, vp, vp], ctypes.c_int),
-        "st_export_words": ([i32], ctypes.c_int),
+        "st_export_env": ([vp, i64, vp, vp, vp, u32, vp, vp], ctypes.c_int),
+        "st_export_words": ([i32, i32], ctypes.c_int),
         "st_gen_actions": ([vp, i64, i64, u64, i64, vp], ctypes.c_int),
         "st_policy_greedy": ([vp, u64, i64, ctypes.c_uint32, vp, vp], ctypes.c_int),
         "st_debug_stamps": ([vp, vp, i64], ctypes.c_int),

@@ -116,12 +116,14 @@ class TetrisEnv:
         L = self.engine._L
         # per-step plumbing without per-call allocations: one device tensor per
         # action value, the step's outputs, and ONE read-back record
-        # (st_export_env: obs words | reward | done | counters | MT words) plus
-        # the image for grayscale / rgb, copied into pinned host buffers and
-        # waited for once
+        # (st_export_env: obs words | reward | done | counters | MT words in
+        # 'global' mode | float32 obs for 'ram') plus the image for grayscale /
+        # rgb, copied into pinned host buffers and waited for once
         self._acts = [torch.full((1,), a, dtype=torch.uint8, device=dev) for a in range(7)]
         self._p_acts = [ctypes.c_void_p(t.data_ptr()) for t in self._acts]
-        self._nrec = int(L.st_export_words(width))
+        self._nrec = int(L.st_export_words(width, height))
+        self._parts = (C.EXPORT_MT if rng == "global" else 0) | (C.EXPORT_OBS_F32 if obs_type == "ram" else 0)
+        self._f32_at = width + 2 + C.NSTAT + C.MT_N  # the record's float32 obs
         self._d_rec = torch.empty(self._nrec, dtype=torch.int32, device=dev)
         self._h_rec = torch.empty(self._nrec, dtype=torch.int32, pin_memory=True)
         self._h_rec_np = self._h_rec.numpy()
@@ -132,7 +134,6 @@ class TetrisEnv:
             self._h_img = torch.empty((1, 84, 84, self._ch), dtype=torch.float32, pin_memory=True)
         self._h_mt = np.zeros(C.MT_N, np.uint32)
         self._h_idx = np.zeros(1, np.int32)
-        self._yb = np.arange(height, dtype=np.uint32)
         # the export and image kernels write straight into the pinned buffers
         # when the runtime maps them for the device (else: device buffer + copy)
         self._rec_dst = _mapped(self._h_rec)
@@ -178,18 +179,20 @@ class TetrisEnv:
 
     def _readback(self, obs_ptr, rew_ptr, done_ptr, prev_idx=None):
         """One read-back per call: the env's record (st_export_env: outputs,
-        counters and CPython's form of its MT state) and, for image
-        observations, its image, each copied to pinned host memory on the
-        stream, then ONE synchronize.  In 'global' mode CPython's random takes
-        the env's MT state if this call drew pieces.  Returns (obs words u32 [W], reward, done, counters int64
-        [NSTAT], image or None)."""
+        counters, CPython's form of its MT state in 'global' mode and the
+        float32 obs for 'ram') and, for image observations, its image, each
+        written to pinned host memory on the stream, then ONE synchronize.
+        In 'global' mode CPython's random takes the env's MT state if this
+        call drew pieces.  Returns (float32 obs [W, H] for 'ram' else None,
+        reward, done, counters [NSTAT] as Python ints, image or None)."""
         eng = self.engine
         L, ctx = eng._L, eng._ctx
         s = self._stream()
         if self._rec_dst is not None:
-            C.check(L.st_export_env(ctx, 0, obs_ptr, rew_ptr, done_ptr, self._rec_dst, s))
+            C.check(L.st_export_env(ctx, 0, obs_ptr, rew_ptr, done_ptr, self._parts, self._rec_dst, s))
         else:
-            C.check(L.st_export_env(ctx, 0, obs_ptr, rew_ptr, done_ptr, ctypes.c_void_p(self._d_rec.data_ptr()), s))
+            C.check(L.st_export_env(ctx, 0, obs_ptr, rew_ptr, done_ptr, self._parts,
+                                    ctypes.c_void_p(self._d_rec.data_ptr()), s))
             C.check(L.st_copy(ctypes.c_void_p(self._h_rec.data_ptr()), ctypes.c_void_p(self._d_rec.data_ptr()),
                               self._nrec * 4, s))
         img = None
@@ -204,18 +207,21 @@ class TetrisEnv:
         self._sync()
         rec = self._h_rec_np
         W = self.width
-        words = rec[:W].view(np.uint32).copy()
+        obs = None
+        if self.obs_type == "ram":  # decoded on the device; a fresh array per step, like np.array(state)
+            a = self._f32_at
+            obs = rec[a:a + W * self.height].view(np.float32).reshape(W, self.height).copy()
         st = rec[W + 2: W + 2 + C.NSTAT].tolist()  # Python ints (the reference's counters are ints)
         if self._rng_mode == "global":
             idx = st[C.STAT["mt_index"]]
             if prev_idx is None or idx != prev_idx or self._rng_sync_state is None:
-                mt = rec[W + 2 + C.NSTAT:].view(np.uint32)
+                mt = rec[W + 2 + C.NSTAT:W + 2 + C.NSTAT + C.MT_N].view(np.uint32)
                 old = random.getstate()
                 random.setstate((old[0], tuple(mt.tolist()) + (idx,), old[2]))
             self._rng_sync_state = random.getstate()
         if img is None and self.obs_type in ("grayscale", "rgb"):
             img = self._h_img.numpy()[0].copy()
-        return words, int(rec[W]), bool(rec[W + 1]), st, img
+        return obs, int(rec[W]), bool(rec[W + 1]), st, img
 
     # ------------------------------------------------------------- gym API
     def _get_info(self, st):
@@ -230,11 +236,10 @@ class TetrisEnv:
                 "deaths": int(st[C.STAT["deaths"]]),
                 "statistics": {SHAPE_NAMES[i]: int(st[c0 + i]) for i in range(7)}}
 
-    def _observation(self, words, img):
+    def _observation(self, obs, img):
         """TetrisEnv._observation (tetris_env.py:413-433) + float32 cast, from
-        the read-back's packed obs words (ram) or image (grayscale / rgb)."""
+        the read-back's float32 obs (ram) or image (grayscale / rgb)."""
         if self.obs_type == "ram":
-            obs = ((words[:, None] >> self._yb[None, :]) & 1).astype(np.float32)
             return obs.reshape(self.width, self.height, 1) if self.extend_dims else obs
         if self.obs_type == "grayscale":
             return img if self.extend_dims else img.reshape(84, 84)
@@ -267,9 +272,9 @@ class TetrisEnv:
         self._push_rng()
         eng = self.engine
         C.check(eng._L.st_step(eng._ctx, self._p_acts[int(action)], self._po, self._pr, self._pd, self._sp))
-        words, r, d, st, img = self._readback(self._po, self._pr, self._pd, prev[C.STAT["mt_index"]])
+        obs, r, d, st, img = self._readback(self._po, self._pr, self._pd, prev[C.STAT["mt_index"]])
         self._stats = st
-        return self._observation(words, img), self._typed_reward(r, d, prev, st), d, self._get_info(st)
+        return self._observation(obs, img), self._typed_reward(r, d, prev, st), d, self._get_info(st)
 
     def reset(self, return_info=False):
         """TetrisEnv.reset (tetris_env.py:405-411): clear(); obs is the empty
@@ -277,9 +282,9 @@ class TetrisEnv:
         self._push_rng()
         C.check(self.engine._L.st_reset(self.engine._ctx, None, self._sp))  # clear() on the env's stream
         self._started = True
-        words, _, _, st, img = self._readback(self._pz, None, None)
+        obs, _, _, st, img = self._readback(self._pz, None, None)
         self._stats = st
-        obs = self._observation(words, img)
+        obs = self._observation(obs, img)
         return (obs, self._get_info(st)) if return_info else obs
 
     def render(self, mode="human"):

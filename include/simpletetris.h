@@ -177,21 +177,26 @@ int st_render(st_ctx *ctx, uint32_t *d_obs, st_stream stream);
 int st_grayscale(st_ctx *ctx, const uint32_t *d_obs, int32_t size, int32_t channels,
                  int32_t as_u8, void *d_out, st_stream stream);
 
-/* One env's step outputs and state as one record of st_export_words(width)
- * uint32 words, for the single-env surface's per-step read-back in ONE
- * transfer (TetrisEnv.step's obs / reward / done and get_info's counters,
+/* One env's step outputs and state as one record of st_export_words(width,
+ * height) uint32 words, for the single-env surface's per-step read-back in
+ * ONE transfer (TetrisEnv.step's obs / reward / done and get_info's counters,
  * tetris_env.py:397-403, :232-241, and CPython's random state, :187):
  *   [0, width)              packed obs word x of `env` (from d_obs [width][n_envs])
  *   width                   reward (from d_reward)      width + 1   done (d_done)
  *   width + 2 + r           stats row r, r < ST_NSTAT (ST_STAT_PIECE: the piece word)
- *   width + 2 + ST_NSTAT + i  MT word i of the env's buffer A, i < 624
- * d_obs / d_reward / d_done may be NULL (zeros written).  The MT words and
- * the ST_STAT_MT_INDEX word are CPython's form (random.getstate(), as
- * st_mt_sync would leave them) without changing the env's state.
- * d_out: device memory (or host memory the device can write). */
+ *   M + i, i < 624          (parts & ST_EXPORT_MT) MT word i, M = width + 2 + ST_NSTAT
+ *   M + 624 + x*height + y  (parts & ST_EXPORT_OBS_F32) cell (x, y) of the obs
+ *                           as float32 0.0 / 1.0: np.array(state, float32), :400
+ * Parts not requested are not written.  d_obs / d_reward / d_done may be
+ * NULL (zeros written).  The MT words and the ST_STAT_MT_INDEX word are
+ * CPython's form (random.getstate(), as st_mt_sync would leave them) without
+ * changing the env's state.  d_out: device memory (or host memory the device
+ * can write). */
+#define ST_EXPORT_MT 1u
+#define ST_EXPORT_OBS_F32 2u
 int st_export_env(st_ctx *ctx, int64_t env, const uint32_t *d_obs, const int32_t *d_reward,
-                  const uint8_t *d_done, uint32_t *d_out, st_stream stream);
-int st_export_words(int32_t width);
+                  const uint8_t *d_done, uint32_t parts, uint32_t *d_out, st_stream stream);
+int st_export_words(int32_t width, int32_t height);
 
 /* Device views of the state (valid until st_destroy). */
 int st_state(st_ctx *ctx, st_state_views *out);

@@ -3,7 +3,8 @@
 #  1. rocprofv3 --kernel-trace --stats of the default bench command (all
 #     variants) and of the headline alone (--no-extras: clean per-kernel stats),
 #     plus tools/trace_summary.py per-run splits of both traces and their
-#     per-kernel@grid JSON -> gpurun_out/${TAG}_trace.json (copy to profiles/)
+#     per-kernel@grid JSON -> profiles/${TAG}_trace.json on the box (so a bench
+#     run after it in the same call reports roofline.rocprof) and gpurun_out/
 #  2. PMC: FETCH_SIZE and WRITE_SIZE in SEPARATE passes (TCC slot limits) over
 #     eager launches of every variant, plus the same two passes over
 #     tools/pmc_calib (known byte counts) -> tools/pmc_summary.py ->
@@ -26,5 +27,6 @@ run rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$TAG" -o fu
  && (cd "$R" && python3 tools/pmc_summary.py "$TAG" "$O/pmc_fetch_$TAG" "$O/pmc_write_$TAG" "$O/pmc_cal_fetch_$TAG" "$O/pmc_cal_write_$TAG" > "$O/pmc_summary_$TAG.json" && cp "profiles/${TAG}_pmc.json" "$O/") \
  && (cd "$R" && python3 tools/trace_summary.py "$O/prof_$TAG/full_kernel_trace.csv" > "$O/trace_summary_$TAG.txt" \
      && python3 tools/trace_summary.py "$O/prof_$TAG/head_kernel_trace.csv" > "$O/trace_summary_head_$TAG.txt" \
-     && python3 tools/trace_summary.py --json "$TAG" "$O/prof_$TAG/head_kernel_trace.csv" "$O/prof_$TAG/full_kernel_trace.csv" > "$O/${TAG}_trace.json") \
+     && python3 tools/trace_summary.py --json "$TAG" "$O/prof_$TAG/head_kernel_trace.csv" "$O/prof_$TAG/full_kernel_trace.csv" > "profiles/${TAG}_trace.json" \
+     && cp "profiles/${TAG}_trace.json" "$O/") \
  && echo "prof ok"

@@ -24,7 +24,7 @@ def step_sync():
     L.st_step(ctx, env._p_acts[3], po, pr, pd, s); hip.hipStreamSynchronize(s)
 t("st_step + hipStreamSynchronize", step_sync)
 def step_export_sync():
-    L.st_step(ctx, env._p_acts[3], po, pr, pd, s); L.st_export_env(ctx, 0, po, pr, pd, env._rec_dst, s); hip.hipStreamSynchronize(s)
+    L.st_step(ctx, env._p_acts[3], po, pr, pd, s); L.st_export_env(ctx, 0, po, pr, pd, env._parts, env._rec_dst, s); hip.hipStreamSynchronize(s)
 t("st_step + export + hipSync", step_export_sync)
 def full():
     if env.step(3)[2]: env.reset()
