@@ -171,6 +171,16 @@ def test_hip_vs_oracle_lock_delay_odd_board():
                                    penalise_height=True, penalise_holes=True, reward_step=True))
 
 
+@pytest.mark.parametrize("W,H", [(4, 4), (32, 28), (5, 27), (31, 6)])
+def test_hip_vs_oracle_extreme_boards(W, H):
+    """The smallest and largest boards st_create accepts (4..32 x 4..28) and
+    lopsided ones, on the generic (runtime W, H) kernel: bit-exact against
+    the oracle over 300 steps with same-step auto-reset (a 4x4 board dies
+    every few steps, so resets and spawns into a full board dominate)."""
+    _oracle_vs_hip(1024, 300, dict(width=W, height=H, advanced_clears=True, penalise_height=True,
+                                   penalise_holes_increase=True), autoreset="same_step")
+
+
 def test_same_step_autoreset_equals_explicit_reset():
     """autoreset='same_step' == 'none' + reset(done) on the same stream."""
     G = _engine()
