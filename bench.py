@@ -106,6 +106,20 @@ def step_grid(n: int) -> int:
     return (n + 63) // 64 * 128
 
 
+def image_launch(n: int, size: int, ch: int, as_u8: bool):
+    """(rocprofv3 kernel name, grid size in threads) of st_grayscale's launch,
+    as launch_grayscale (st_kernels.hip) picks it: float32 rgb in sweep order
+    (at most 1,024 blocks of 4 waves, 4 1-KB runs per wave iteration), else
+    2 envs per 256-thread block."""
+    t = "unsigned char" if as_u8 else "float"
+    V = 16 if as_u8 else 4
+    per = size * size * ch
+    if not as_u8 and ch == 3 and 64 * V * 4 <= per and (n * per) % V == 0:
+        runs = (n * per + 64 * V - 1) // (64 * V)
+        return f"k_grayscale_sweep<{t}, {ch}>", min((runs + 15) // 16, 1024) * 256
+    return f"k_grayscale<{t}, {ch}>", (n + 1) // 2 * 256
+
+
 def load_pmc(kname: str, sha: str):
     """Per-launch HBM bytes (FETCH+WRITE, gfx950-corrected by
     tools/pmc_summary.py) of `kname` (`name@grid`: that kernel at that grid
@@ -573,10 +587,11 @@ def image_variants(head, C, timed, roofline, dev, s, sp, W, WU, K):
         el, ev, _ = timed(eng, run_img, KG)
         kern_us = ev * 1e3 / KG
         bpe = 4 * W + 84 * 84 * ch * 4
+        kname, grid = image_launch(n, 84, ch, False)
         r = {"kernel_only": True, "launches": KG, "kernel_us": kern_us,
-             "roofline": roofline(kern_us, bpe, n, f"k_grayscale<float, {ch}>",
+             "roofline": roofline(kern_us, bpe, n, kname,
                                   {"bytes_formula": f"read packed obs 4W + write 84*84*{ch}*4 per env"},
-                                  grid=(n + 15) // 16 * 256)}  # launch_grayscale: 16 envs per 256-thread block
+                                  grid=grid)}
         # whole steps with this obs_type: st_step + the image per step
         KS = max(1, min(K, 100))
 

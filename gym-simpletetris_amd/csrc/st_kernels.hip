@@ -1699,7 +1699,17 @@ __global__ __launch_bounds__(256) void k_export(KParams p, int64_t env, const ui
 // each chunk's elements are decoded from the block's packed obs words staged
 // in LDS.  Reads are 4 B per env per board column, coalesced over the
 // block's envs.
-constexpr int kImgEnvs = 16;  // envs per block: 64-B obs row segments
+// 2 envs per block: the blocks' regions are 2 x 28 KB (grayscale 84 f32), so
+// the concurrently written regions sit closer together than with 16 envs
+// (tools/ab_img.py at 65,536 envs: 84 gray f32 386 -> 356 us, 160 rgb u8
+// 2,350 -> 2,072 us; tools/write_bw.hip shows the same effect on bare stores)
+#ifndef ST_IMG_ENVS
+#define ST_IMG_ENVS 2
+#endif
+#ifndef ST_IMG_SWEEP
+#define ST_IMG_SWEEP 1
+#endif
+constexpr int kImgEnvs = ST_IMG_ENVS;  // envs per block
 constexpr int kMaxImg = 4096;  // largest image side (st_grayscale checks)
 
 template <typename T>
@@ -1852,6 +1862,145 @@ __global__ __launch_bounds__(256) void k_grayscale(const uint32_t *__restrict__ 
             const int p = rem / channels;
             base[f] = pix(le, p / size, p - (p / size) * size);
         }
+    }
+}
+
+// The same images in sweep order: the grid strides over the WHOLE output, so
+// that all waves write within one moving window of the image batch
+// (tools/write_bw.hip: 16-B non-temporal store sweeps reach 5.8-6.0 TB/s with
+// 128-1,024 workgroups, against 4.8-5.3 TB/s when every block owns a region
+// of 16 .. 1 envs).  It pays for float32 rgb only: the per-element decode
+// (two table reads and a lane shuffle) keeps the grayscale and u8 sweeps
+// below the per-block kernel.  Per iteration a wave writes U
+// consecutive 1-KB runs (64 lanes x 16 B); the U runs span at most two envs
+// (64 V U <= size^2 CH, checked by the launcher), whose packed obs words the
+// wave fetches once per iteration (one word per lane, the next iteration's
+// prefetched under the current one's stores) and hands to each element with
+// a lane shuffle.
+#ifndef ST_IMG_GRID
+#define ST_IMG_GRID 1024
+#endif
+constexpr int kImgRuns = 4;  // U: 1-KB runs per wave iteration
+template <typename T, int CH>
+__global__ __launch_bounds__(256) void k_grayscale_sweep(const uint32_t *__restrict__ obs, T *__restrict__ out,
+                                                         int64_t n, int W, int H, int size) {
+    __shared__ int8_t RM[kMaxImg], CM[kMaxImg];
+    const int lim = W > H ? W : H;
+    const int gap = size / 100 + 1;
+    const int blk = (size - 2 * gap) / lim - gap;
+    const int pitch = blk + gap;
+    const int pr = (size - (gap + pitch * H)) / 2;
+    const int pc = (size - (gap + pitch * W)) / 2;
+    for (int i = threadIdx.x; i < size; i += blockDim.x) {
+        const int r = i - pr, c = i - pc;
+        RM[i] = (int8_t)((r < 0 || r >= gap + pitch * H) ? -2 : (r % pitch < gap ? -1 : r / pitch));
+        CM[i] = (int8_t)((c < 0 || c >= gap + pitch * W) ? -2 : (c % pitch < gap ? -1 : c / pitch));
+    }
+    __syncthreads();
+    constexpr int V = 16 / (int)sizeof(T);  // elements per 16-B chunk
+    constexpr int U = kImgRuns;
+    constexpr int RUN = kWave * V;  // elements per 1-KB run
+    const int lane = threadIdx.x & (kWave - 1);
+    const int per = size * size * CH;
+    const int64_t total = n * (int64_t)per;
+    // a position as (env, row, column, channel) digits, advanced by fixed
+    // element counts without runtime division
+    struct Pos {
+        int64_t l;
+        int r, c, k;
+    };
+    struct Step {
+        int64_t l;
+        int r, c, k;
+    };
+    auto mkstep = [&](int64_t d) -> Step {
+        const int64_t l = d / per;
+        const int q = (int)(d - l * per);
+        const int p = q / CH;
+        return Step{l, p / size, p % size, q - p * CH};
+    };
+    auto adv = [&](Pos x, const Step &d) -> Pos {
+        x.k += d.k;
+        if (x.k >= CH) {
+            x.k -= CH;
+            ++x.c;
+        }
+        x.c += d.c;
+        if (x.c >= size) {
+            x.c -= size;
+            ++x.r;
+        }
+        x.r += d.r;
+        if (x.r >= size) {
+            x.r -= size;
+            ++x.l;
+        }
+        x.l += d.l;
+        return x;
+    };
+    const int64_t S = (int64_t)gridDim.x * (blockDim.x / kWave) * U * RUN;  // elements per grid iteration
+    const Step dS = mkstep(S), dR = mkstep(RUN);
+    const int64_t gw = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+    int64_t f = gw * (U * RUN) + (int64_t)lane * V;
+    Pos pos;
+    {
+        const Step s0 = mkstep(f);
+        pos = Pos{s0.l, s0.r, s0.c, s0.k};
+    }
+    // this lane's word slot: env (lane / W) of the pair, column lane % W
+    const int wx = lane % W, we = lane / W;
+    const bool wlane = lane < 2 * W;
+    auto fetch = [&](int64_t ea) -> uint32_t {
+        const int64_t e = ea + we;
+        return (wlane && e < n) ? obs[(int64_t)wx * n + e] : 0u;
+    };
+    auto first = [](int64_t v) -> int64_t {  // the wave's lowest-f active lane holds its lowest env
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+        return (int64_t)(((uint64_t)hi << 32) | lo);
+    };
+    int64_t ea = first(pos.l);
+    uint32_t wcur = f < total ? fetch(ea) : 0u;
+    for (; f < total; f += S) {
+        const Pos nxt = adv(pos, dS);
+        const bool more = f + S < total;
+        const int64_t ean = first(more ? nxt.l : ea);
+        const uint32_t wnext = more ? fetch(ean) : 0u;  // prefetch under this iteration's stores
+        Pos q = pos;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t fu = f + (int64_t)u * RUN;
+            if (fu < total) {
+                T v[V];
+                int jk = q.k, jc = q.c, jr = q.r;
+                int64_t jl = q.l;
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    const int y = RM[jr], x = CM[jc];
+                    const int src = (int)(jl - ea) * W + (x < 0 ? 0 : x);
+                    const uint32_t w = (uint32_t)__shfl((int)wcur, src);
+                    const uint32_t px = (y == -2 || x == -2) ? 0u
+                                        : (y < 0 || x < 0) ? 128u
+                                        : (((w >> y) & 1u) ? 190u : 128u);
+                    v[j] = (T)px;
+                    if (CH == 1 || ++jk == CH) {
+                        jk = 0;
+                        if (++jc == size) {
+                            jc = 0;
+                            if (++jr == size) {
+                                jr = 0;
+                                ++jl;
+                            }
+                        }
+                    }
+                }
+                store16_nt(out + fu, v);
+            }
+            if (u + 1 < U) q = adv(q, dR);
+        }
+        pos = nxt;
+        ea = ean;
+        wcur = wnext;
     }
 }
 
@@ -2021,6 +2170,31 @@ hipError_t launch_obs_f32(const KParams &p, const uint32_t *obs, float *out, hip
 hipError_t launch_grayscale(const KParams &p, const uint32_t *obs, int size, int channels,
                             int as_u8, void *out, hipStream_t s) {
     if (p.n <= 0) return hipSuccess;
+    // float32 rgb in sweep order (84 rgb f32 at 65,536 envs: 1,035 us against
+    // 1,105 us per 2-env block; grayscale and u8 measured faster per block:
+    // 356 vs 405 us, 2,072 vs 3,265 us), when a wave iteration's U 1-KB runs
+    // span at most two envs and the output is 16-B aligned; else per block
+    const int V = as_u8 ? 16 : 4;
+    const int64_t per = (int64_t)size * size * channels;
+    if (ST_IMG_SWEEP && !as_u8 && channels == 3 && kWave * V * kImgRuns <= per &&
+        (reinterpret_cast<uintptr_t>(out) & 15u) == 0 && (p.n * per) % V == 0) {
+        const int64_t runs = (p.n * per + kWave * V - 1) / (kWave * V);
+        const int64_t want = (runs + 4 * kImgRuns - 1) / (4 * kImgRuns);  // 4 waves per block
+        const dim3 grid((unsigned)(want < ST_IMG_GRID ? want : ST_IMG_GRID)), block(256);
+        if (as_u8 && channels == 3)
+            hipLaunchKernelGGL((k_grayscale_sweep<uint8_t, 3>), grid, block, 0, s, obs, (uint8_t *)out, p.n, p.W,
+                               p.H, size);
+        else if (as_u8)
+            hipLaunchKernelGGL((k_grayscale_sweep<uint8_t, 1>), grid, block, 0, s, obs, (uint8_t *)out, p.n, p.W,
+                               p.H, size);
+        else if (channels == 3)
+            hipLaunchKernelGGL((k_grayscale_sweep<float, 3>), grid, block, 0, s, obs, (float *)out, p.n, p.W,
+                               p.H, size);
+        else
+            hipLaunchKernelGGL((k_grayscale_sweep<float, 1>), grid, block, 0, s, obs, (float *)out, p.n, p.W,
+                               p.H, size);
+        return hipGetLastError();
+    }
     const dim3 grid((unsigned)((p.n + kImgEnvs - 1) / kImgEnvs)), block(256);
     if (as_u8 && channels == 3)
         hipLaunchKernelGGL((k_grayscale<uint8_t, 3>), grid, block, 0, s, obs, (uint8_t *)out, p.n, p.W, p.H, size);

@@ -173,6 +173,11 @@ def test_bench_roofline_bytes_and_pmc_tie():
     tr = bench.load_trace(kname, tj["kernel_source_sha"])
     assert tr["launches"] == tj["kernels"][kname]["launches"] and tr["source"] == "r02_trace.json"
     assert bench.load_trace(kname, "0" * 16) is None
+    # the image kernels' launch keys as bench.py derives them are the ones the
+    # PMC pass recorded (launch_grayscale's choice of kernel and grid)
+    for ch in (1, 3):
+        key = "%s@%d" % bench.image_launch(65536, 84, ch, False)
+        assert key in d["kernels"], key
     # the committed profiles describe the committed kernel sources
     assert d["kernel_source_sha"] == tj["kernel_source_sha"] == bench.kernel_source_sha()
 

@@ -283,10 +283,12 @@ def _image_np(cols, W, H, size):
 
 @pytest.mark.parametrize("n", [1, 17, 1000])
 def test_image_kernels_ragged_batches(n):
-    """st_grayscale / st_obs_to_f32 over ragged batches (16-env and 64-env
-    blocks with a partial last block), every size / channel / dtype path."""
+    """st_grayscale / st_obs_to_f32 over ragged batches, every size / channel
+    / dtype path: the sweep-order image kernel (a wave's 64 chunks within two
+    envs) and the per-block one it falls back to (tiny images: 4x4 boards at
+    sizes 12-18, and u8 totals that are not a multiple of 16 B)."""
     G = _engine()
-    for (W, H) in ((10, 20), (7, 13)):
+    for (W, H, sizes) in ((10, 20, (84, 160, 50)), (7, 13, (84, 160, 50)), (4, 4, (12, 16, 18))):
         b = G.TetrisBatch(n, width=W, height=H, seeds=range(n), autoreset="same_step")
         b.reset()
         for t in range(30):
@@ -295,7 +297,7 @@ def test_image_kernels_ragged_batches(n):
         f32 = b.obs_to_f32().cpu().numpy()
         ref = ((cols[:, :, None] >> np.arange(H, dtype=np.uint64)) & 1).astype(np.float32)
         assert np.array_equal(f32, ref), (W, H)
-        for size in (84, 160, 50):
+        for size in sizes:
             exp = _image_np(cols, W, H, size)
             for ch in (1, 3):
                 for u8 in (False, True):
