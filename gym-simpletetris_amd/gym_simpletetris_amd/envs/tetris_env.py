@@ -176,6 +176,7 @@ class TetrisEnv:
                           C.MT_N * 4, s))
         C.check(L.st_copy(ctypes.c_void_p(v.stats + C.STAT["mt_index"] * v.stride * 4),
                           ctypes.c_void_p(self._h_idx.ctypes.data), 4, s))
+        self._rng_sync_state = state  # the device now mirrors CPython's state
 
     def _readback(self, obs_ptr, rew_ptr, done_ptr, prev_idx=None):
         """One read-back per call: the env's record (st_export_env: outputs,
@@ -214,11 +215,14 @@ class TetrisEnv:
         st = rec[W + 2: W + 2 + C.NSTAT].tolist()  # Python ints (the reference's counters are ints)
         if self._rng_mode == "global":
             idx = st[C.STAT["mt_index"]]
+            # the cached state is CPython's current one (_push_rng checked it
+            # before the step); only a step that drew changes it
             if prev_idx is None or idx != prev_idx or self._rng_sync_state is None:
                 mt = rec[W + 2 + C.NSTAT:W + 2 + C.NSTAT + C.MT_N].view(np.uint32)
-                old = random.getstate()
-                random.setstate((old[0], tuple(mt.tolist()) + (idx,), old[2]))
-            self._rng_sync_state = random.getstate()
+                old = self._rng_sync_state if self._rng_sync_state is not None else random.getstate()
+                new = (old[0], tuple(mt.tolist()) + (idx,), old[2])
+                random.setstate(new)
+                self._rng_sync_state = new
         if img is None and self.obs_type in ("grayscale", "rgb"):
             img = self._h_img.numpy()[0].copy()
         return obs, int(rec[W]), bool(rec[W + 1]), st, img

@@ -352,6 +352,59 @@ def test_single_env_surface_vs_reference(name, rng):
     env.close()
 
 
+def test_single_env_global_rng_with_user_draws():
+    """TetrisEnv(rng='global') while the program also uses `random` between
+    steps (random(), randint(), a re-seed mid-run): every step and the final
+    random.getstate() equal the oracle driven by one shared CPython state --
+    the reference's behaviour, where the env's draws and the user's
+    interleave on the global MT (tetris_env.py:187)."""
+    G = _engine()
+    kw = dict(advanced_clears=True, penalise_holes_increase=True)
+    acts = np.random.default_rng(5).integers(0, 7, 400)
+
+    def user(t, rnd):
+        if t % 37 == 5:
+            rnd.random()
+        if t % 53 == 7:
+            rnd.randint(0, 9)
+        if t == 200:
+            rnd.seed(99)
+
+    random.seed(11)
+    env = G.TetrisEnv(rng="global", **kw)
+    env.reset()
+    got = []
+    for t, a in enumerate(acts):
+        user(t, random)
+        o, r, d, _ = env.step(int(a))
+        got.append((o.copy(), r, d))
+        if d:
+            env.reset()
+    final = random.getstate()
+    env.close()
+
+    R = random.Random(11)  # the same program on the oracle, one CPython state throughout
+    ob = O.OracleBatch(1, [0], **kw)
+
+    def oracle_call(fn):
+        mt, idx = R.getstate()[1][:624], R.getstate()[1][624]
+        ob.envs[0].rng.mt[:] = mt
+        ob.envs[0].rng.index = idx
+        out = fn()
+        old = R.getstate()
+        R.setstate((old[0], tuple(int(x) for x in ob.envs[0].rng.mt) + (int(ob.envs[0].rng.index),), old[2]))
+        return out
+    oracle_call(lambda: ob.reset(0))
+    for t, a in enumerate(acts):
+        user(t, R)
+        o, r, d, _ = oracle_call(lambda: ob.step_one(0, int(a)))
+        assert np.array_equal(got[t][0], o.astype(np.float32)), t
+        assert got[t][1] == r and got[t][2] == d, t
+        if d:
+            oracle_call(lambda: ob.reset(0))
+    assert final == R.getstate()
+
+
 def test_single_env_errors_and_render():
     G = _engine()
     env = G.make("SimpleTetris-v0", rng="private", seed=3)
