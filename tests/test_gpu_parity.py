@@ -1,6 +1,7 @@
 """HIP engine parity: the C-ABI library (libsimpletetris.so) on the GPU vs the
 reference's own outputs (tests/golden/*.npz) and the C oracle.  Bit-exact for
 every field (integer / bit work: no tolerance)."""
+import ctypes
 import random
 
 import numpy as np
@@ -403,6 +404,51 @@ def test_single_env_global_rng_with_user_draws():
         if d:
             oracle_call(lambda: ob.reset(0))
     assert final == R.getstate()
+
+
+def test_export_env_any_env_every_part():
+    """st_export_env on envs 0, 37 and n-1 of a running batch, all parts: the
+    record equals the step's outputs, the counters and MT state that
+    st_mt_sync then produces (the export itself changes nothing), and the
+    float32 obs equals the packed words unpacked; parts not asked for stay
+    untouched; bad arguments are refused."""
+    G = _engine()
+    from gym_simpletetris_amd import _lib as C
+    n, W, H = 300, 10, 20
+    b = G.TetrisBatch(n, seeds=range(n), autoreset="same_step", advanced_clears=True)
+    b.reset()
+    for t in range(200):
+        o, r, d = b.step(b.gen_actions(t, 5))
+    L, ctx = b._L, b._ctx
+    sp = ctypes.c_void_p(torch.cuda.current_stream(b.device).cuda_stream)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    nw = L.st_export_words(W, H)
+    assert nw == W + 2 + C.NSTAT + C.MT_N + W * H
+    recs = {}
+    for env in (0, 37, n - 1):
+        rec = torch.zeros(nw, dtype=torch.int32, device=b.device)
+        C.check(L.st_export_env(ctx, env, P(o), P(r), P(d), C.EXPORT_MT | C.EXPORT_OBS_F32, P(rec), sp))
+        recs[env] = rec.cpu().numpy()
+    words = o.cpu().numpy().view(np.uint32)
+    rew, done = r.cpu().numpy(), d.cpu().numpy()
+    st = b.get_state(("stats", "mt"))  # st_mt_sync: the canonical form the export computed read-only
+    m = W + 2 + C.NSTAT
+    for env, rec in recs.items():
+        assert np.array_equal(rec[:W].view(np.uint32), words[:, env]), env
+        assert rec[W] == rew[env] and rec[W + 1] == int(done[env]), env
+        assert np.array_equal(rec[W + 2:m], st["stats"][:, env]), env
+        assert np.array_equal(rec[m:m + C.MT_N].view(np.uint32), st["mt"][env]), env
+        f32 = rec[m + C.MT_N:].view(np.float32).reshape(W, H)
+        bits = ((words[:, env][:, None].astype(np.uint64) >> np.arange(H, dtype=np.uint64)) & 1).astype(np.float32)
+        assert np.array_equal(f32, bits), env
+    rec = torch.full((nw,), -7, dtype=torch.int32, device=b.device)
+    C.check(L.st_export_env(ctx, 5, P(o), P(r), P(d), 0, P(rec), sp))
+    h = rec.cpu().numpy()
+    assert (h[m:] == -7).all() and np.array_equal(h[:W].view(np.uint32), words[:, 5])
+    for env, parts in ((n, 0), (-1, 0), (0, 4)):
+        with pytest.raises(C.StError):
+            C.check(L.st_export_env(ctx, env, P(o), P(r), P(d), parts, P(rec), sp))
+    b.close()
 
 
 def test_single_env_errors_and_render():
