@@ -30,6 +30,11 @@ from .. import spaces
 from ..engine import SHAPE_NAMES, TetrisBatch
 
 
+# counter rows of the export record (st_stat)
+_TIME, _SCORE, _LINES, _HOLES, _DEATHS, _HEIGHT, _C0, _PIECE = (
+    C.STAT[k] for k in ("time", "score", "lines", "holes", "deaths", "piece_height", "count0", "piece"))
+
+
 def _obs_space(obs_type, width, height, extend_dims):
     """tetris_env.py:381-392."""
     if obs_type == "ram":
@@ -228,17 +233,17 @@ class TetrisEnv:
         return obs, int(rec[W]), bool(rec[W + 1]), st, img
 
     # ------------------------------------------------------------- gym API
-    def _get_info(self, st):
-        """TetrisEngine.get_info (tetris_env.py:232-241)."""
-        pw = int(st[C.STAT["piece"]]) & 0xFFFFFFFF
-        c0 = C.STAT["count0"]
-        return {"time": int(st[C.STAT["time"]]),
-                "current_piece": SHAPE_NAMES[pw & 7],
-                "score": int(st[C.STAT["score"]]),
-                "lines_cleared": int(st[C.STAT["lines"]]),
-                "holes": int(st[C.STAT["holes"]]),
-                "deaths": int(st[C.STAT["deaths"]]),
-                "statistics": {SHAPE_NAMES[i]: int(st[c0 + i]) for i in range(7)}}
+    @staticmethod
+    def _get_info(st):
+        """TetrisEngine.get_info (tetris_env.py:232-241); `st` holds Python
+        ints (the record's counter rows, .tolist())."""
+        return {"time": st[_TIME],
+                "current_piece": SHAPE_NAMES[st[_PIECE] & 7],
+                "score": st[_SCORE],
+                "lines_cleared": st[_LINES],
+                "holes": st[_HOLES],
+                "deaths": st[_DEATHS],
+                "statistics": dict(zip(SHAPE_NAMES, st[_C0:_C0 + 7]))}
 
     def _observation(self, obs, img):
         """TetrisEnv._observation (tetris_env.py:413-433) + float32 cast, from
@@ -253,12 +258,10 @@ class TetrisEnv:
         """Reproduce the Python type the reference's reward ends up with (R18)."""
         if done:
             return int(r)
-        c0 = C.STAT["count0"]
-        locked = sum(st[c0:c0 + 7]) > sum(prev[c0:c0 + 7])
-        if not locked:
+        if st[_C0:_C0 + 7] == prev[_C0:_C0 + 7]:  # no new piece: the step did not lock
             return int(r)
         if self._scoring["advanced_clears"]:
-            hp = C.STAT["piece_height"]
+            hp = _HEIGHT
             if self._scoring["penalise_height"] or (
                     self._scoring["penalise_height_increase"] and st[hp] > prev[hp]):
                 return np.float64(r)
