@@ -350,6 +350,10 @@ class TetrisVecEnv:
     terminal observation (what the reference's step returned) and
     info['ep_score'] / ['ep_lines'] / ['ep_time'] / ['ep_holes'] hold the
     finished episode's counters.  Buffers are reused between steps.
+    Actions outside 0..6 raise KeyError like the reference's; for actions
+    already on the GPU that check is one device->host sync per step, which
+    `validate_actions=False` removes (the loop then stays asynchronous;
+    out-of-range values act as idle).
     """
 
     def __init__(self, num_envs: int, width=10, height=20, obs_type="ram", extend_dims=False,
@@ -357,7 +361,7 @@ class TetrisVecEnv:
                  advanced_clears=False, high_scoring=False, penalise_holes=False,
                  penalise_holes_increase=False, lock_delay=0, step_reset=False, *,
                  device=None, seed: int = 0, global_offset: int = 0, autoreset: bool = True,
-                 obs_format: str = "f32"):
+                 obs_format: str = "f32", validate_actions: bool = True):
         if obs_format not in ("f32", "packed"):
             raise ValueError("obs_format must be 'f32' or 'packed'")
         self.num_envs = int(num_envs)
@@ -370,7 +374,8 @@ class TetrisVecEnv:
                                   advanced_clears=advanced_clears, high_scoring=high_scoring,
                                   penalise_holes=penalise_holes,
                                   penalise_holes_increase=penalise_holes_increase,
-                                  autoreset="same_step" if autoreset else "none", device=device)
+                                  autoreset="same_step" if autoreset else "none", device=device,
+                                  validate_actions=validate_actions)
         self.engine.seed([seed + global_offset + e for e in range(self.num_envs)])
         self.single_action_space = spaces.Discrete(7)
         self.single_observation_space = _obs_space(obs_type, width, height, extend_dims)

@@ -532,6 +532,25 @@ def test_vec_env_surface():
     assert not torch.equal(v.engine.info_tensors()["time"], live["time"])
 
 
+def test_vec_env_unvalidated_actions():
+    """validate_actions=False: no check (no sync); an out-of-range action acts
+    as idle (action 6), in-range ones as usual; the default raises KeyError."""
+    G = _engine()
+    n = 512
+    a = G.TetrisVecEnv(n, seed=4, validate_actions=False, obs_format="packed")
+    b = G.TetrisVecEnv(n, seed=4, obs_format="packed")
+    a.reset()
+    b.reset()
+    g = torch.Generator(device="cpu").manual_seed(0)
+    for t in range(60):
+        acts = torch.randint(0, 10, (n,), dtype=torch.uint8, generator=g).to(a.device)
+        oa, ra, da, _ = a.step(acts)
+        ob, rb, db, _ = b.step(torch.where(acts > 6, torch.full_like(acts, 6), acts))
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
+    with pytest.raises(KeyError):
+        b.step(torch.full((n,), 7, dtype=torch.uint8, device=b.device))
+
+
 @pytest.mark.parametrize("autoreset", ["same_step", "none"])
 @pytest.mark.parametrize("board", [(10, 20), (9, 15)])
 def test_rollout_equals_steps(autoreset, board):
