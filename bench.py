@@ -516,6 +516,7 @@ def main():
         variants.update(image_variants(head, C, timed, roofline, dev, s, sp, W, WU, K))
         if world == 1:
             variants["single_env"] = single_env_variant(2000)
+            variants["vec_env"] = vec_env_variant(args.n_envs, 1000, dev)
         if not args.no_clear_heavy and not f32:
             variants["step_clear_heavy"] = clear_heavy(head, cfg_kw, C, ShardedTetris, timed, roofline,
                                                        kname_of, dev, s, sp, rank, world, W, H, K, WU,
@@ -560,6 +561,33 @@ def single_env_variant(steps: int):
     out["reference_us_per_step"] = {"ram": 1e6 / REF_PY_STEPS_PER_S, "grayscale": 1e6 / 8052,
                                     "note": "reference TetrisEnv.step(), 1 core of the build container "
                                             "(SURVEY §6), incl. reset on done"}
+    return out
+
+
+def vec_env_variant(n: int, steps: int, dev):
+    """The batched Python surface (TetrisVecEnv.step, the vector counterpart
+    of tetris_env.py:397-403) with actions already on the GPU, as an RL loop
+    calls it: wall time per step, packed and float32 obs, with and without
+    the per-step action check (one device->host sync)."""
+    from gym_simpletetris_amd.envs.tetris_env import TetrisVecEnv
+    out = {}
+    for fmt in ("packed", "f32"):
+        for val in (False, True):
+            v = TetrisVecEnv(n, seed=1000, obs_format=fmt, validate_actions=val, device=dev)
+            v.reset()
+            acts = torch.randint(0, 7, (64, n), dtype=torch.uint8, device=dev)
+            for t in range(50):
+                v.step(acts[t % 64])
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for t in range(steps):
+                v.step(acts[t % 64])
+            torch.cuda.synchronize(dev)
+            dt = (time.perf_counter() - t0) / steps
+            out[f"{fmt}/validate_actions={val}"] = {"us_per_step": dt * 1e6, "env_steps_per_s": n / dt}
+            v.close()
+    out["note"] = ("TetrisVecEnv.step incl. the per-step info snapshot; host-bound above the kernel "
+                   "(DESIGN.md §5.1)")
     return out
 
 
