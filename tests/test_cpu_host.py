@@ -31,6 +31,20 @@ def test_library_exports_every_header_symbol():
     assert set(names) == set(_lib.EXPORTS)
 
 
+def test_host_only_abi_functions_and_constants():
+    """The C ABI's pure host functions (no GPU call) and the header constants
+    the Python binding mirrors."""
+    from gym_simpletetris_amd import _lib
+    L = _lib.load()
+    assert L.st_abi_version() == 1
+    assert L.st_export_words(10, 20) == 10 + 2 + _lib.NSTAT + _lib.MT_N + 200
+    assert L.st_export_words(4, 4) == 4 + 2 + _lib.NSTAT + _lib.MT_N + 16
+    src = open(os.path.join(ROOT, "include", "simpletetris.h")).read()
+    defs = dict(re.findall(r"#define\s+(ST_EXPORT_\w+)\s+(\d+)u", src))
+    assert int(defs["ST_EXPORT_MT"]) == _lib.EXPORT_MT and int(defs["ST_EXPORT_OBS_F32"]) == _lib.EXPORT_OBS_F32
+    assert int(re.search(r"\bST_NSTAT\s*=\s*(\d+)", src).group(1)) == _lib.NSTAT  # enum constant
+
+
 def test_library_is_gfx950_code_object():
     from gym_simpletetris_amd import _lib
     data = open(_lib.LIB_PATH, "rb").read()
