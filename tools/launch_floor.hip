@@ -59,7 +59,10 @@ static float time_graph(dim3 g, dim3 b, size_t lds, hipStream_t s, int K) {
     return ms * 1000.f / K;
 }
 
-int main() {
+int main(int argc, char **argv) {
+    // "eager": eager launches only (a run under rocprofv3 --kernel-trace: the
+    // traced duration of an empty kernel is the tracer's per-dispatch share)
+    const bool eager_only = argc > 1 && argv[1][0] == 'e';
     hipStream_t s;
     CHECK(hipStreamCreate(&s));
     const int K = 2000;
@@ -69,7 +72,7 @@ int main() {
         for (auto sh : shapes)
             for (size_t lds : {(size_t)0, (size_t)16384}) {
                 const float e = time_eager(dim3(sh.wg), dim3(sh.th), lds, s, K);
-                const float g = time_graph(dim3(sh.wg), dim3(sh.th), lds, s, K);
+                const float g = eager_only ? 0.f : time_graph(dim3(sh.wg), dim3(sh.th), lds, s, K);
                 printf("{\"workgroups\": %d, \"threads\": %d, \"lds\": %zu, \"eager_us\": %.3f, \"graph_us\": %.3f}\n",
                        sh.wg, sh.th, lds, e, g);
             }
