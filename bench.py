@@ -247,6 +247,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="headline only (profiling passes)")
     ap.add_argument("--no-clear-heavy", action="store_true")
+    ap.add_argument("--no-surfaces", action="store_true",
+                    help="skip the Python-surface timings (single_env, vec_env): PMC passes, whose "
+                         "per-kernel averages would otherwise mix in their launches")
     ap.add_argument("--gather-steps", type=int, default=200)
     args = ap.parse_args()
 
@@ -514,7 +517,7 @@ def main():
         variants["c2"]["config"] = f"C2: 4096 boards per GPU, {args.config.upper()} rewards"
         w.close()
         variants.update(image_variants(head, C, timed, roofline, dev, s, sp, W, WU, K))
-        if world == 1:
+        if world == 1 and not args.no_surfaces:
             variants["single_env"] = single_env_variant(2000)
             variants["vec_env"] = vec_env_variant(args.n_envs, 1000, dev)
         if not args.no_clear_heavy and not f32:
@@ -567,12 +570,13 @@ def single_env_variant(steps: int):
 def vec_env_variant(n: int, steps: int, dev):
     """The batched Python surface (TetrisVecEnv.step, the vector counterpart
     of tetris_env.py:397-403) with actions already on the GPU, as an RL loop
-    calls it: wall time per step, packed and float32 obs, with and without
-    the per-step action check (one device->host sync)."""
+    calls it: wall time per step, packed and float32 obs, without the action
+    check, with it on the GPU ('async': st_check_actions, no sync) and with
+    the per-step device->host check."""
     from gym_simpletetris_amd.envs.tetris_env import TetrisVecEnv
     out = {}
     for fmt in ("packed", "f32"):
-        for val in (False, True):
+        for val in (False, "async", True):
             v = TetrisVecEnv(n, seed=1000, obs_format=fmt, validate_actions=val, device=dev)
             v.reset()
             acts = torch.randint(0, 7, (64, n), dtype=torch.uint8, device=dev)

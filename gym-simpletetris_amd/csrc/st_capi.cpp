@@ -407,6 +407,13 @@ int st_policy_greedy(st_ctx *c, uint64_t seed, int64_t t, uint32_t explore_permi
     return ST_OK;
 }
 
+int st_check_actions(const uint8_t *d_actions, int64_t n, uint32_t *d_flag, st_stream stream) {
+    if (n < 0) return fail(ST_EINVAL, "st_check_actions: negative size");
+    if (n > 0 && (!d_actions || !d_flag)) return fail(ST_EINVAL, "st_check_actions: null argument");
+    ST_HIP(st::launch_check_actions(d_actions, n, d_flag, (hipStream_t)stream));
+    return ST_OK;
+}
+
 int st_gen_actions(uint8_t *d_out, int64_t n, int64_t t, uint64_t seed, int64_t global_offset,
                    st_stream stream) {
     if (!d_out && n > 0) return fail(ST_EINVAL, "st_gen_actions: null output");

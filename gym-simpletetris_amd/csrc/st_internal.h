@@ -67,6 +67,7 @@ hipError_t launch_policy_greedy(const KParams &p, uint64_t seed, int64_t t, uint
                                 uint8_t *out, hipStream_t s);
 hipError_t launch_grayscale(const KParams &p, const uint32_t *obs, int size, int channels,
                             int as_u8, void *out, hipStream_t s);
+hipError_t launch_check_actions(const uint8_t *a, int64_t n, uint32_t *flag, hipStream_t s);
 hipError_t launch_gen_actions(uint8_t *out, int64_t n, int64_t t, uint64_t seed, int64_t off,
                               hipStream_t s);
 

@@ -2018,6 +2018,25 @@ __global__ void k_gen_actions(uint8_t *out, int64_t n, int64_t t, uint64_t seed,
     out[e] = (uint8_t)(splitmix64(x) % 7ull);
 }
 
+// st_check_actions: a sticky flag for actions outside 0..6 (the reference's
+// KeyError, tetris_env.py:245), 16 actions per lane from one 16-B load.  A
+// byte b is > 6 iff b >= 0x80 or (b & 0x7F) + 0x79 reaches bit 7 (no carry
+// leaves the byte).  Only lanes that saw one store the flag (vector stores).
+__global__ __launch_bounds__(256) void k_check_actions(const uint8_t *__restrict__ a, int64_t n,
+                                                       uint32_t *flag) {
+    const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+    if (i0 >= n) return;
+    bool bad = false;
+    if (i0 + 16 <= n && (reinterpret_cast<uintptr_t>(a + i0) & 15u) == 0) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(a + i0);
+        auto over6 = [](uint32_t w) { return ((((w & 0x7F7F7F7Fu) + 0x79797979u) | w) & 0x80808080u) != 0u; };
+        bad = over6(v.x) || over6(v.y) || over6(v.z) || over6(v.w);
+    } else {
+        for (int64_t i = i0; i < n && i < i0 + 16; ++i) bad = bad || a[i] > 6;
+    }
+    if (bad) flag[0] = 1u;
+}
+
 // ---------------------------------------------------------------- greedy policy
 // Benchmark / test workload generator (not part of the reference env): the
 // action a greedy placement player takes in every env's current state, so
@@ -2211,6 +2230,13 @@ hipError_t launch_policy_greedy(const KParams &p, uint64_t seed, int64_t t, uint
                                 uint8_t *out, hipStream_t s) {
     hipLaunchKernelGGL(k_policy_greedy, dim3((unsigned)(p.stride / kWave)), dim3(kWave), 0, s, p, seed, t,
                        explore, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_check_actions(const uint8_t *a, int64_t n, uint32_t *flag, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_check_actions, dim3((unsigned)((n + 16 * 256 - 1) / (16 * 256))), dim3(256), 0, s, a,
+                       n, flag);
     return hipGetLastError();
 }
 

@@ -39,6 +39,18 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[ctypes.c_void_p]:
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+def _mapped(t: torch.Tensor):
+    """Device address of a pinned host tensor (hipHostGetDevicePointer), or
+    None if the runtime does not map it for the device."""
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        dp = ctypes.c_void_p()
+        rc = hip.hipHostGetDevicePointer(ctypes.byref(dp), ctypes.c_void_p(t.data_ptr()), 0)
+        return dp if rc == 0 and dp.value else None
+    except OSError:
+        return None
+
+
 def _from_dlpack(x):
     """A foreign device array (any DLPack producer: __dlpack__ /
     __dlpack_device__, e.g. a learner's action buffer) as a torch tensor over
@@ -91,8 +103,20 @@ class TetrisBatch:
         # step()/rollout() reject actions outside 0..6 like the reference's
         # value_action_map[action] KeyError (tetris_env.py:245).  For a device
         # tensor that check costs one device->host sync per call;
-        # validate_actions=False skips it (values >= 7 then act as idle).
-        self.validate_actions = bool(validate_actions)
+        # validate_actions=False skips it (values >= 7 then act as idle), and
+        # 'async' checks on the device (st_check_actions into a sticky flag in
+        # mapped host memory) without a sync: the KeyError comes at the next
+        # step()/rollout() after the flag is seen, or from check_actions().
+        if validate_actions not in (True, False, "async"):
+            raise ValueError("validate_actions must be True, False or 'async'")
+        self.validate_actions = validate_actions
+        self._flag_h = self._flag_dev = None
+        if validate_actions == "async":
+            self._flag_h = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._flag_np = self._flag_h.numpy()
+            self._flag_dev = _mapped(self._flag_h)
+            if self._flag_dev is None:
+                raise RuntimeError("validate_actions='async' needs pinned host memory mapped for the device")
         cfg = C.Config(self.width, self.height, self.lock_delay, flags, C.AUTORESET[autoreset])
         ctx = ctypes.c_void_p()
         with torch.cuda.device(device):
@@ -159,9 +183,12 @@ class TetrisBatch:
         7): the reference raises KeyError for an action outside
         value_action_map (tetris_env.py:152-160, :245)."""
         shape = tuple(lead) + (self.n,)
-        if (not self.validate_actions and type(x) is torch.Tensor and x.dtype == torch.uint8
+        if (self.validate_actions is not True and type(x) is torch.Tensor and x.dtype == torch.uint8
                 and x.device == self.device and x.is_contiguous() and tuple(x.shape) == shape):
-            return x  # an RL loop's own device buffer: nothing to check or convert
+            if self.validate_actions == "async":  # an RL loop's own device buffer, checked on the GPU
+                self._raise_flagged()
+                C.check(self._L.st_check_actions(_ptr(x), x.numel(), self._flag_dev, self._stream()))
+            return x
         x = _from_dlpack(x)
         if isinstance(x, torch.Tensor):
             if x.dtype.is_floating_point or x.dtype == torch.bool or x.is_complex():
@@ -185,6 +212,20 @@ class TetrisBatch:
             v = a.flat[np.flatnonzero((a < 0) | (a > 6))[0]]
             raise KeyError(f"action {v} not in 0..6 (tetris_env.py:245)")
         return torch.as_tensor(a.astype(np.uint8).reshape(shape), device=self.device)
+
+    def _raise_flagged(self):
+        if self._flag_np[0]:
+            self._flag_np[0] = 0
+            raise KeyError("an action outside 0..6 reached an earlier step (validate_actions='async'; "
+                           "tetris_env.py:245); it acted as idle")
+
+    def check_actions(self):
+        """validate_actions='async': wait for the work queued so far and raise
+        KeyError if any checked action was outside 0..6."""
+        if self.validate_actions != "async":
+            return
+        torch.cuda.current_stream(self.device).synchronize()
+        self._raise_flagged()
 
     def reset(self, mask=None):
         """TetrisEngine.clear() on every env (mask None) or where mask != 0."""

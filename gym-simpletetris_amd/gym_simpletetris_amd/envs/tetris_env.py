@@ -27,7 +27,7 @@ import torch
 
 from .. import _lib as C
 from .. import spaces
-from ..engine import SHAPE_NAMES, TetrisBatch
+from ..engine import SHAPE_NAMES, TetrisBatch, _mapped
 
 
 # counter rows of the export record (st_stat)
@@ -65,18 +65,6 @@ def _stream_sync(sp: ctypes.c_void_p, device):
     except (OSError, AttributeError):
         stream = torch.cuda.current_stream(device)
         return stream.synchronize
-
-
-def _mapped(t: torch.Tensor):
-    """Device address of a pinned host tensor (hipHostGetDevicePointer), or
-    None if the runtime does not map it for the device."""
-    try:
-        hip = ctypes.CDLL("libamdhip64.so")
-        dp = ctypes.c_void_p()
-        rc = hip.hipHostGetDevicePointer(ctypes.byref(dp), ctypes.c_void_p(t.data_ptr()), 0)
-        return dp if rc == 0 and dp.value else None
-    except OSError:
-        return None
 
 
 class TetrisEnv:
@@ -353,7 +341,8 @@ class TetrisVecEnv:
     Actions outside 0..6 raise KeyError like the reference's; for actions
     already on the GPU that check is one device->host sync per step, which
     `validate_actions=False` removes (the loop then stays asynchronous;
-    out-of-range values act as idle).
+    out-of-range values act as idle) and `validate_actions='async'` moves to
+    the GPU (the KeyError then comes at a later step or check_actions()).
     """
 
     def __init__(self, num_envs: int, width=10, height=20, obs_type="ram", extend_dims=False,
@@ -404,6 +393,11 @@ class TetrisVecEnv:
         out = self.engine.step(actions, obs="f32" if want_f32 else "packed")
         f32 = out[0] if want_f32 else None
         return self._obs(self.engine.obs, f32), out[1], out[2], VecInfo(self.engine)
+
+    def check_actions(self):
+        """validate_actions='async': raise KeyError if an action outside 0..6
+        reached any step so far (waits for the queued work)."""
+        self.engine.check_actions()
 
     def close(self):
         self.engine.close()

@@ -250,6 +250,13 @@ int st_policy_greedy(st_ctx *ctx, uint64_t seed, int64_t t, uint32_t explore_per
 int st_gen_actions(uint8_t *d_out, int64_t n, int64_t t, uint64_t seed,
                    int64_t global_offset, st_stream stream);
 
+/* Sticky check for actions outside 0..6 (the reference raises KeyError for
+ * them, tetris_env.py:245; st_step treats them as idle): sets *d_flag = 1 if
+ * any of d_actions[0..n) is > 6, never clears it.  d_flag may be host memory
+ * mapped for the device, so the caller can poll it without synchronising
+ * (the batched surface's validate_actions='async'). */
+int st_check_actions(const uint8_t *d_actions, int64_t n, uint32_t *d_flag, st_stream stream);
+
 /* Diagnostics: when the environment variable ST_STAMPS is set at st_create,
  * st_step runs an instrumented build of the step kernel that records
  * s_memtime at its phase boundaries per wave; this copies the last step's

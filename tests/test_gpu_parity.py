@@ -551,6 +551,54 @@ def test_vec_env_unvalidated_actions():
         b.step(torch.full((n,), 7, dtype=torch.uint8, device=b.device))
 
 
+def test_async_action_check():
+    """validate_actions='async': st_check_actions flags an out-of-range
+    action on the GPU without a sync; the KeyError comes at the next step
+    after the flag is seen (or from check_actions()), and the steps equal
+    unvalidated ones.  st_check_actions itself: every byte position, the
+    unaligned / ragged tail path, values 7 and 255."""
+    G = _engine()
+    from gym_simpletetris_amd import _lib as C
+    n = 1000
+    a = G.TetrisBatch(n, seeds=range(n), autoreset="same_step", validate_actions="async")
+    b = G.TetrisBatch(n, seeds=range(n), autoreset="same_step", validate_actions=False)
+    a.reset()
+    b.reset()
+    for t in range(20):
+        acts = b.gen_actions(t, 3).clone()
+        oa, ra, da = a.step(acts)
+        ob, rb, db = b.step(acts)
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
+    a.check_actions()  # nothing flagged
+    bad = b.gen_actions(99, 3).clone()
+    bad[617] = 9
+    a.step(bad)  # no sync, no error yet
+    torch.cuda.synchronize()
+    with pytest.raises(KeyError):
+        a.step(b.gen_actions(100, 3))
+    a.step(b.gen_actions(101, 3))  # the flag was cleared
+    a.check_actions()
+    a.step(bad)
+    with pytest.raises(KeyError):
+        a.check_actions()
+    # the kernel on its own
+    L = a._L
+    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    flag = torch.zeros(1, dtype=torch.int32, device=a.device)
+    buf = torch.zeros(4096 + 16, dtype=torch.uint8, device=a.device)
+    for length, off in ((4096, 0), (4096, 1), (37, 3), (1, 0)):
+        for pos in sorted({0, length // 2, length - 1}):
+            for v in (6, 7, 255):
+                buf.zero_()
+                flag.zero_()
+                buf[off + pos] = v
+                C.check(L.st_check_actions(ctypes.c_void_p(buf.data_ptr() + off), length,
+                                           ctypes.c_void_p(flag.data_ptr()), sp))
+                assert int(flag.item()) == (1 if v > 6 else 0), (length, off, pos, v)
+    a.close()
+    b.close()
+
+
 @pytest.mark.parametrize("autoreset", ["same_step", "none"])
 @pytest.mark.parametrize("board", [(10, 20), (9, 15)])
 def test_rollout_equals_steps(autoreset, board):

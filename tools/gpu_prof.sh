@@ -6,10 +6,14 @@
 #     per-kernel@grid JSON -> profiles/${TAG}_trace.json on the box (so a bench
 #     run after it in the same call reports roofline.rocprof) and gpurun_out/
 #  2. PMC: FETCH_SIZE and WRITE_SIZE in SEPARATE passes (TCC slot limits) over
-#     eager launches of every variant, plus the same two passes over
+#     eager launches of every kernel variant (not the Python-surface timings,
+#     whose launches of the same kernels would mix into the averages), plus
+#     the same two passes over
 #     tools/pmc_calib (known byte counts) -> tools/pmc_summary.py ->
 #     gpurun_out/${TAG}_pmc.json (copy to profiles/)
-# Every GPU step has its own time limit; steps are chained with &&.
+# Every GPU step has its own time limit; steps are chained with &&.  The raw
+# trace / counter CSVs are deleted once summarised (gpurun copies back at most
+# 64 MiB of gpurun_out/).
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd /tmp && export TMPDIR=/tmp
@@ -20,8 +24,8 @@ B="$R/bench.py"
 run() { echo "== $*"; timeout -k 10 400 "$@"; }
 run rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$TAG" -o full -- python3 $B --no-cpu-baseline > "$O/prof_bench_$TAG.json" 2> "$O/prof_$TAG.err" \
  && run rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$TAG" -o head -- python3 $B --no-extras > "$O/prof_head_$TAG.json" 2>> "$O/prof_$TAG.err" \
- && run rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$O/pmc_fetch_$TAG" -o packed -- python3 $B --no-cpu-baseline --steps 600 --warmup 100 --launch eager --rollout-chunk 50 > /dev/null 2>> "$O/prof_$TAG.err" \
- && run rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$O/pmc_write_$TAG" -o packed -- python3 $B --no-cpu-baseline --steps 600 --warmup 100 --launch eager --rollout-chunk 50 > /dev/null 2>> "$O/prof_$TAG.err" \
+ && run rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$O/pmc_fetch_$TAG" -o packed -- python3 $B --no-cpu-baseline --no-surfaces --steps 600 --warmup 100 --launch eager --rollout-chunk 50 > /dev/null 2>> "$O/prof_$TAG.err" \
+ && run rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$O/pmc_write_$TAG" -o packed -- python3 $B --no-cpu-baseline --no-surfaces --steps 600 --warmup 100 --launch eager --rollout-chunk 50 > /dev/null 2>> "$O/prof_$TAG.err" \
  && run rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$O/pmc_cal_fetch_$TAG" -o cal -- "$R/tools/pmc_calib" >> "$O/prof_$TAG.err" 2>&1 \
  && run rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$O/pmc_cal_write_$TAG" -o cal -- "$R/tools/pmc_calib" >> "$O/prof_$TAG.err" 2>&1 \
  && (cd "$R" && python3 tools/pmc_summary.py "$TAG" "$O/pmc_fetch_$TAG" "$O/pmc_write_$TAG" "$O/pmc_cal_fetch_$TAG" "$O/pmc_cal_write_$TAG" > "$O/pmc_summary_$TAG.json" && cp "profiles/${TAG}_pmc.json" "$O/") \
@@ -29,4 +33,6 @@ run rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$TAG" -o fu
      && python3 tools/trace_summary.py "$O/prof_$TAG/head_kernel_trace.csv" > "$O/trace_summary_head_$TAG.txt" \
      && python3 tools/trace_summary.py --json "$TAG" "$O/prof_$TAG/head_kernel_trace.csv" "$O/prof_$TAG/full_kernel_trace.csv" > "profiles/${TAG}_trace.json" \
      && cp "profiles/${TAG}_trace.json" "$O/") \
+ && find "$O/prof_$TAG" "$O/pmc_fetch_$TAG" "$O/pmc_write_$TAG" "$O/pmc_cal_fetch_$TAG" "$O/pmc_cal_write_$TAG" \
+      -name "*.csv" ! -name "*_stats.csv" -delete \
  && echo "prof ok"

@@ -15,7 +15,7 @@ import gym_simpletetris_amd as G  # noqa: E402
 n, T = 65536, int(sys.argv[1]) if len(sys.argv) > 1 else 2000
 out = {}
 for fmt in ("packed", "f32"):
-    for val in (False, True):
+    for val in (False, "async", True):
         v = G.TetrisVecEnv(n, seed=1000, obs_format=fmt, validate_actions=val)
         v.reset()
         acts = torch.randint(0, 7, (64, n), dtype=torch.uint8, device=v.device)
