@@ -53,13 +53,14 @@ class ParallelOracle:
             ob.reset()
         self.pool = ThreadPoolExecutor(len(self.sl))
 
-    def rollout(self, t0, T):
+    def rollout(self, t0, T, obs=True):
         def one(i):
             a, b = self.sl[i]
             acts = O.splitmix64_actions(ASEED, t0, T, b - a, offset=a)
-            return self.obs[i].rollout(acts, want_obs=True, want_stats=False)
+            return self.obs[i].rollout(acts, want_obs=obs, want_stats=False)
         rs = list(self.pool.map(one, range(len(self.sl))))
-        return {k: np.concatenate([r[k] for r in rs], axis=1) for k in ("reward", "done", "obs")}
+        keys = ("reward", "done", "obs") if obs else ("reward", "done")
+        return {k: np.concatenate([r[k] for r in rs], axis=1) for k in keys}
 
     def final_state(self):
         """Structured view of every env (Env struct fields) in global order."""
@@ -242,6 +243,42 @@ def test_ragged_and_large_batches(n, steps):
             _compare(t0, rew[t0:t0 + T].cpu().numpy(), done[t0:t0 + T].cpu().numpy(),
                      obs[t0:t0 + T].cpu().numpy().view(np.uint32), ref)
         _check_final(eng, orc)
+    finally:
+        orc.close()
+        eng.close()
+
+
+def test_soak_many_generations():
+    """100,000 steps of 8,192 envs (st_rollout, 1,000 steps per launch): ~40
+    MT generation switches and ~1,800 episodes per env; every step's
+    reward and done, then the final board / piece / counters / MT state,
+    bit-exact against the oracle (C4 scoring)."""
+    import gym_simpletetris_amd as G
+    n, T, CH = 8192, 100000, 1000
+    kw = CONFIGS["c4"]
+    eng = G.TetrisBatch(n, autoreset="same_step", seeds=[SEED_BASE + e for e in range(n)],
+                        width=W, height=H, **kw)
+    eng.reset()
+    orc = ParallelOracle(n, kw)
+    acts = torch.empty((CH, n), dtype=torch.uint8, device=eng.device)
+    try:
+        deaths = 0
+        for t0 in range(0, T, CH):
+            for t in range(CH):
+                eng.gen_actions(t0 + t, ASEED, out=acts[t])
+            _, r, d = eng.rollout(acts, obs="none")
+            ref = orc.rollout(t0, CH, obs=False)
+            assert np.array_equal(r.cpu().numpy(), ref["reward"]), f"reward, steps {t0}.."
+            dn = d.cpu().numpy().astype(np.uint8)
+            assert np.array_equal(dn, ref["done"]), f"done, steps {t0}.."
+            deaths += int(dn.sum())
+        _check_final(eng, orc)
+        assert deaths > 1000 * n  # the episodes really turned over
+        fin = orc.final_state()["rng"]["mt"].astype(np.uint32)
+        gen = _twist_np(_seeded_words(n))
+        for _ in range(12):  # far past them: none of the first twelve generations remains
+            assert not (fin == gen).all(axis=1).any()
+            gen = _twist_np(gen)
     finally:
         orc.close()
         eng.close()
