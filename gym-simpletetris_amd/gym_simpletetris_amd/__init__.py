@@ -7,6 +7,15 @@ the single-env reference surface; `make('SimpleTetris-v0', num_envs=N, ...)`
 or `make('SimpleTetrisVec-v0', ...)` the batched one.  When gym or gymnasium
 is importable the ids are registered there too.
 """
+import os as _os
+
+# Kernel arguments in device memory for every launch: the step is one short
+# launch per env-step, and this measured 1-5% faster per step on MI355X
+# (DESIGN §5.1).  HIP reads it once, when its runtime starts, so it applies
+# when this package is imported before anything touches the GPU; an explicit
+# setting in the environment wins.
+_os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 from .engine import SHAPE_NAMES, TetrisBatch  # noqa: F401
 from .envs import TetrisEnv, TetrisVecEnv  # noqa: F401
 
