@@ -38,7 +38,8 @@ sys.path.insert(0, os.path.join(ROOT, "gym-simpletetris_amd"))
 sys.path.insert(0, ROOT)
 # kernel arguments in device memory (as the package sets it; must precede the
 # HIP runtime's start): profiles/r02_ab_env.txt, DESIGN §5.1
-os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+if not os.environ.get("HIP_FORCE_DEV_KERNARG"):
+    os.environ["HIP_FORCE_DEV_KERNARG"] = "1"
 
 import torch  # noqa: E402  (importing torch does not initialise the GPU)
 import torch.distributed as dist  # noqa: E402

@@ -13,8 +13,9 @@ import os as _os
 # launch per env-step, and this measured 1-5% faster per step on MI355X
 # (DESIGN §5.1).  HIP reads it once, when its runtime starts, so it applies
 # when this package is imported before anything touches the GPU; an explicit
-# setting in the environment wins.
-_os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+# non-empty setting in the environment wins (HIP reads an empty one as 0).
+if not _os.environ.get("HIP_FORCE_DEV_KERNARG"):
+    _os.environ["HIP_FORCE_DEV_KERNARG"] = "1"
 
 from .engine import SHAPE_NAMES, TetrisBatch  # noqa: F401
 from .envs import TetrisEnv, TetrisVecEnv  # noqa: F401
