@@ -36,9 +36,13 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gym-simpletetris_amd"))
 sys.path.insert(0, ROOT)
-# kernel arguments in device memory (as the package sets it; must precede the
-# HIP runtime's start): profiles/r02_ab_env.txt, DESIGN §5.1
-if not os.environ.get("HIP_FORCE_DEV_KERNARG"):
+# Kernel arguments in device memory (HIP_FORCE_DEV_KERNARG=1): the package's
+# documented opt-in (gym_simpletetris_amd.tune_runtime(); importing it sets
+# nothing), which bench.py takes before the HIP runtime starts, as a
+# step-per-launch user would (profiles/r02_ab_env.txt).  An
+# explicit setting in the environment wins; the line records which applied.
+KERNARG_FROM_ENV = bool(os.environ.get("HIP_FORCE_DEV_KERNARG"))
+if not KERNARG_FROM_ENV:
     os.environ["HIP_FORCE_DEV_KERNARG"] = "1"
 
 import torch  # noqa: E402  (importing torch does not initialise the GPU)
@@ -124,11 +128,18 @@ def image_launch(n: int, size: int, ch: int, as_u8: bool):
     return f"k_grayscale<{t}, {ch}>", (n + 1) // 2 * 256
 
 
+def launch_key(kname: str, grid: int, k: int) -> str:
+    """The key a profile summary files a launch under: kernel name, grid size
+    in threads and steps per launch (1 for st_step, K for st_rollout), so a
+    number is only ever reported beside a run of the same launch shape."""
+    return f"{kname}@{grid}@k{k}"
+
+
 def load_pmc(kname: str, sha: str):
     """Per-launch HBM bytes (FETCH+WRITE, gfx950-corrected by
-    tools/pmc_summary.py) of `kname` (`name@grid`: that kernel at that grid
-    size) from a committed profiles/*_pmc.json whose kernel-source hash equals
-    the running sources'; (None, reason) if none."""
+    tools/pmc_summary.py) of `kname` (launch_key: that kernel at that grid
+    size and steps per launch) from a committed profiles/*_pmc.json whose
+    kernel-source hash equals the running sources'; (None, reason) if none."""
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), reverse=True):
         try:
             d = json.load(open(f))
@@ -139,13 +150,14 @@ def load_pmc(kname: str, sha: str):
         v = d.get("kernels", {}).get(kname)
         if v is not None:
             return v.get("hbm_bytes_per_launch"), os.path.basename(f)
-    return None, f"no PMC pass of these kernel sources (sha {sha}) under profiles/"
+    return None, f"no PMC pass of these kernel sources (sha {sha}) at this launch shape ({kname}) under profiles/"
 
 
 def load_trace(kname: str, sha: str):
-    """rocprofv3 kernel-trace duration stats of `kname` (`name@grid`, the
-    longest run of launches) from a committed profiles/*_trace.json
-    (tools/trace_summary.py --json) of the same kernel sources; None if none."""
+    """rocprofv3 kernel-trace duration stats of `kname` (launch_key, the
+    longest run of launches, with the p_lock of the traced bench run) from a
+    committed profiles/*_trace.json (tools/trace_summary.py --json) of the
+    same kernel sources; None if none."""
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_trace.json")), reverse=True):
         try:
             d = json.load(open(f))
@@ -174,8 +186,11 @@ def cpu_baseline(seconds: float, config: str):
     """The C oracle (a restatement of the reference step; the Python reference
     cannot travel to the GPU box) on a bounded sample of the same workload:
     4,096 envs per process, same seeds/actions, auto-reset.  One process on one
-    core, then one process per available core (capped at the box's 16-core
-    share) at once; `value` is the all-cores aggregate."""
+    core, then one process per core of this process's CPU share at once;
+    `value` is the aggregate.  The share: the affinity mask, capped by
+    OMP_NUM_THREADS when the harness sets it (the GPU box exports 16 = its
+    CPU share per GPU, while nproc / the affinity mask show all the host's
+    cores, which other jobs use)."""
     cmd = [sys.executable, "-m", "oracle.cpu_bench", "--envs", "4096", "--seconds", str(seconds),
            "--config", config]
 
@@ -191,14 +206,21 @@ def cpu_baseline(seconds: float, config: str):
     one = result(launch(0))
     single = one["env_steps"] / one["seconds"]
     avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    P = max(1, min(16, avail))
+    share = avail
+    try:
+        share = min(avail, int(os.environ["OMP_NUM_THREADS"]))
+        why = f"OMP_NUM_THREADS={share} (the harness's CPU share; affinity mask {avail})"
+    except (KeyError, ValueError):
+        why = f"affinity mask ({avail} cores)"
+    P = max(1, share)
     rs = [result(pr) for pr in [launch(p) for p in range(P)]]
     agg = sum(r["env_steps"] / r["seconds"] for r in rs)
     return dict(value=agg, unit="env-steps/s", cores=P, kind="port",
-                single_core=single, nproc=os.cpu_count(), cores_available=avail, cpu_model=cpu_model(),
-                sample=f"C oracle (oracle/tetris_oracle.c) on {P} processes x 4096 envs, "
-                       f"{rs[0]['steps']} steps each in ~{seconds:.0f} s (aggregate of per-process "
-                       f"rates); 1 process alone: {single:.4g} env-steps/s ({one['steps']} steps)",
+                per_core=agg / P, single_core=single, nproc=os.cpu_count(), cores_available=avail,
+                cores_basis=why, cpu_model=cpu_model(),
+                sample=f"C oracle (oracle/tetris_oracle.c) on {P} processes x 4096 envs (one per core of "
+                       f"the share: {why}), {rs[0]['steps']} steps each in ~{seconds:.0f} s (aggregate of "
+                       f"per-process rates); 1 process alone: {single:.4g} env-steps/s ({one['steps']} steps)",
                 reference_python_1core_build_container=REF_PY_STEPS_PER_S)
 
 
@@ -319,7 +341,11 @@ def main():
     def timed(eng, run, nsteps):
         """Time `run()` (enqueues exactly nsteps steps of `eng` on s): barrier +
         synchronize on both sides, max over ranks; events on s give the GPU
-        span.  p_lock from the spawn counters (every lock spawns one piece)."""
+        span.  p_lock from the spawn counters (every lock spawns one piece),
+        read after everything enqueued before the region has finished (the
+        counters are read on the current stream; work still queued on s
+        would race them)."""
+        torch.cuda.synchronize(dev)
         c0 = spawned(eng)
         with torch.cuda.stream(s):  # s is current for the whole region (graph replay launches on it)
             ev0.record(s)  # first host calls after a stream switch are slow: not inside the region
@@ -353,25 +379,49 @@ def main():
             return f"k_step<10, 20, {b(f32)}, false, {b(sc0)}>"
         return f"k_rollout<10, 20, {b(f32)}, {b(sc0)}>"
 
-    def roofline(kern_us, bpe, units_per_launch, kname, extra=None, grid=None):
+    def roofline(ev_us, bpe, units_per_launch, kname, extra=None, grid=None, k=1, bytes_at=None):
+        """Roofline object of one launch shape: `achieved` = algorithmic bytes
+        per launch / the HIP-event time per launch of the timed region (the
+        contract's live measurement; at small K it includes the region's ramp);
+        `traffic` and `rocprof` only from committed profiles of the same
+        kernel sources AND launch shape (kernel, grid, steps per launch),
+        else null with the reason.  bytes_at(p_lock) re-prices the bytes at
+        the traced run's own p_lock for the rocprof fraction."""
         bpl = bpe * units_per_launch
-        achieved = bpl / (kern_us * 1e-6) / 1e9
-        if grid is None:
+        achieved = bpl / (ev_us * 1e-6) / 1e9
+        key = launch_key(kname, grid, k) if grid is not None else None
+        if key is None:
             traffic, src = None, "not collected for this variant"
         else:
-            traffic, src = load_pmc(f"{kname}@{grid}", sha)
+            traffic, src = load_pmc(key, sha)
         r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
-             "kernel_us": kern_us, "bytes_per_env_step": bpe, "bytes_per_launch": bpl,
+             "frac": achieved / HBM_PEAK_GBS,
+             "frac_basis": "bytes_per_launch / (HIP-event span of the timed region / launches)",
+             "traffic": traffic, "kernel": kname, "launch_key": key,
+             "event_us_per_launch": ev_us, "bytes_per_env_step": bpe, "bytes_per_launch": bpl,
              "traffic_source": src, "kernel_source_sha": sha}
-        tr = load_trace(f"{kname}@{grid}", sha) if grid is not None else None
-        if tr is not None:  # the committed rocprofv3 trace of the same sources
+        tr = load_trace(key, sha) if key is not None else None
+        if tr is not None:  # the committed rocprofv3 trace of the same sources and launch shape
+            pl = tr.get("p_lock")
+            bpl_tr = bytes_at(pl) * units_per_launch if (bytes_at and pl is not None) else bpl
             r["rocprof"] = {"mean_us": tr["mean_us"], "median_us": tr["median_us"],
                             "launches": tr["launches"], "source": f"{tr['source']} ({tr['trace']})",
-                            "frac_at_traced_mean": bpl / (tr["mean_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS}
+                            "p_lock_traced_run": pl, "bytes_per_launch_traced_run": bpl_tr,
+                            "frac_at_traced_mean": bpl_tr / (tr["mean_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                            "frac_at_traced_median": bpl_tr / (tr["median_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS}
         if extra:
             r.update(extra)
         return r
+
+    def action_rows(eng_gen, offset, n, t0, T, have):
+        """Action rows t0 .. t0+T-1 of the synthetic stream for this shard: a
+        slice of `have` (rows 0..len-1) when it holds them, else generated."""
+        if have is not None and t0 + T <= have.shape[0]:
+            return have[t0:t0 + T]
+        a = torch.empty((T, n), dtype=torch.uint8, device=dev)
+        for t in range(T):
+            eng_gen(t0 + t, aseed, global_offset=offset, out=a[t])
+        return a
 
     class Workload:
         """One engine shard + its K+W action rows + reused output buffers."""
@@ -417,23 +467,38 @@ def main():
             torch.cuda.synchronize(dev)
             return g.replay, g
 
-        def measure(self):
+        def steady(self, S=1000):
+            """After the timed region: S more launches back to back (action
+            rows reused cyclically), HIP events around them only -- the
+            kernel's launch-to-launch period without the region's ramp (the
+            first launch after an idle GPU, the final synchronize)."""
+            rows = list(range(WU, WU + K))
+            el, ev_ms, p_lock = timed(self.eng, lambda: [self.launch(rows[i % len(rows)]) for i in range(S)], S)
+            return ev_ms * 1e3 / S, p_lock
+
+        def measure(self, steady=True):
             self.warmup()
             run, keep = self.runner()
             el, ev_ms, p_lock = timed(self.eng, run, K)
             del keep
-            kern_us = ev_ms * 1e3 / K
+            ev_us = ev_ms * 1e3 / K
             kname = kname_of("step", self.f32, self.sc0)
-            rl = roofline(kern_us, s8d_bytes(p_lock, self.f32), self.n_local, kname, grid=step_grid(self.n_local),
-                          extra={
+            bytes_at = lambda pl: s8d_bytes(pl, self.f32)  # noqa: E731
+            rl = roofline(ev_us, s8d_bytes(p_lock, self.f32), self.n_local, kname, grid=step_grid(self.n_local),
+                          k=1, bytes_at=bytes_at, extra={
                 "bytes_formula": "SURVEY 8(d): %d + 184 p_lock" % (902 if self.f32 else 182),
-                "frac_s8d": s8d_bytes(p_lock, self.f32) * self.n_local / (kern_us * 1e3) / HBM_PEAK_GBS,
                 "bytes_per_env_step_layout": algorithmic_bytes(W, H, p_lock, self.f32),
                 "frac_layout": algorithmic_bytes(W, H, p_lock, self.f32) * self.n_local
-                / (kern_us * 1e3) / HBM_PEAK_GBS,
+                / (ev_us * 1e3) / HBM_PEAK_GBS,
                 "p_lock": p_lock})
             if rl["traffic"] is not None:
                 rl["traffic_over_layout_bytes"] = rl["traffic"] / (rl["bytes_per_env_step_layout"] * self.n_local)
+            if steady:
+                st_us, st_pl = self.steady()
+                rl["steady"] = {"launches": 1000, "event_us_per_launch": st_us, "p_lock": st_pl,
+                                "frac": s8d_bytes(st_pl, self.f32) * self.n_local / (st_us * 1e3) / HBM_PEAK_GBS,
+                                "basis": "1,000 further launches back to back after the timed region, "
+                                         "HIP events around them (no region ramp / final synchronize)"}
             return {"value": self.n_global * K / el, "ms_per_step": el / K * 1e3,
                     "event_ms_per_step": ev_ms / K, "p_lock": p_lock, "roofline": rl}
 
@@ -469,6 +534,8 @@ def main():
             "launch": ("hipGraph of K st_step launches" if args.launch == "graph"
                        else "K eager st_step launches"),
             "parallelism": f"env-shard x{world}",
+            "hip_force_dev_kernarg": os.environ.get("HIP_FORCE_DEV_KERNARG"),
+            "hip_force_dev_kernarg_from": "environment" if KERNARG_FROM_ENV else "bench.py (tune_runtime opt-in)",
         },
         "p_lock": hm["p_lock"],
         "event_ms_per_step": hm["event_ms_per_step"],
@@ -481,43 +548,48 @@ def main():
         L, ctx = eng._L, eng._ctx
         if not f32:  # the same st_step with the reference's float32 obs fused in
             w = Workload(args.n_envs, cfg_kw, True)
-            variants["step_f32"] = w.measure()
+            variants["step_f32"] = w.measure(steady=False)
             w.close()
-        # K-step rollout kernel (st_rollout), continuing the headline's state
-        CH = min(args.rollout_chunk, K)
-        nch = K // CH
+        # K-step rollout kernel (st_rollout), continuing the headline's state:
+        # a fixed CH steps per launch whatever K is (so its PMC / trace keys
+        # match the profiles' launch shape), max(1, K // CH) timed launches
+        CH = args.rollout_chunk
+        nch = max(1, K // CH)
         n_local = head.n_local
         ro = torch.empty((CH, W, n_local), dtype=torch.int32, device=dev)
         rr = torch.empty((CH, n_local), dtype=torch.int32, device=dev)
         rd = torch.empty((CH, n_local), dtype=torch.uint8, device=dev)
+        racts = action_rows(eng.gen_actions, head.sh.offset, n_local, WU, (nch + 1) * CH, head.actions)
         for use_f32 in (False, True):
             rf = torch.empty((CH, n_local, W, H), dtype=torch.float32, device=dev) if use_f32 else None
-            aptr = [ctypes.c_void_p(head.actions[WU + c * CH].data_ptr()) for c in range(nch)]
+            aptr = [ctypes.c_void_p(racts[c * CH].data_ptr()) for c in range(nch + 1)]
             ptrs = [ctypes.c_void_p(x.data_ptr()) if x is not None else None for x in (ro, rf, rr, rd)]
 
             def run_ro():
-                for c in range(nch):
+                for c in range(1, nch + 1):
                     C.check(L.st_rollout(ctx, CH, aptr[c], *ptrs, sp))
-            with torch.cuda.stream(s):  # warm-up launch
+            with torch.cuda.stream(s):  # warm-up launch (timed() waits for it before reading counters)
                 C.check(L.st_rollout(ctx, CH, aptr[0], *ptrs, sp))
             el, ev, pl = timed(eng, run_ro, nch * CH)
-            kern_us = ev * 1e3 / nch
+            ev_us = ev * 1e3 / nch
             variants["rollout_f32" if use_f32 else "rollout_packed"] = {
                 "value": head.n_global * nch * CH / el, "ms_per_step": el / (nch * CH) * 1e3,
-                "steps_per_launch": CH, "p_lock": pl,
-                "roofline": roofline(kern_us, rollout_bytes(W, H, pl, use_f32, CH), CH * n_local,
-                                     kname_of("rollout", use_f32, head.sc0), grid=step_grid(n_local), extra=
+                "steps_per_launch": CH, "launches": nch, "p_lock": pl,
+                "roofline": roofline(ev_us, rollout_bytes(W, H, pl, use_f32, CH), CH * n_local,
+                                     kname_of("rollout", use_f32, head.sc0), grid=step_grid(n_local), k=CH,
+                                     bytes_at=lambda q, f=use_f32: rollout_bytes(W, H, q, f, CH), extra=
                                      {"bytes_formula": "rollout: I/O per step + state r/w per launch / K",
                                       "p_lock": pl})}
             del rf
+        del racts
         # the other single-GPU BASELINE configs: C2 (4,096 boards), C4 / C3
         other = "c3" if args.config == "c4" else "c4"
         w = Workload(args.n_envs, CONFIGS[other], f32)
-        variants[other] = w.measure()
+        variants[other] = w.measure(steady=False)
         variants[other]["config"] = f"{other.upper()} at {args.n_envs} boards per GPU"
         w.close()
         w = Workload(4096, cfg_kw, f32)
-        variants["c2"] = w.measure()
+        variants["c2"] = w.measure(steady=False)
         variants["c2"]["config"] = f"C2: 4096 boards per GPU, {args.config.upper()} rewards"
         w.close()
         variants.update(image_variants(head, C, timed, roofline, dev, s, sp, W, WU, K))
@@ -575,8 +647,9 @@ def vec_env_variant(n: int, steps: int, dev):
     """The batched Python surface (TetrisVecEnv.step, the vector counterpart
     of tetris_env.py:397-403) with actions already on the GPU, as an RL loop
     calls it: wall time per step, packed and float32 obs, without the action
-    check, with it on the GPU ('async': st_check_actions, no sync) and with
-    the per-step device->host check."""
+    check, with the step kernel's own check ('async', the default: a sticky
+    flag in mapped host memory, st_set_action_flag; no extra launch, no sync)
+    and with the per-step device->host check (True)."""
     from gym_simpletetris_amd.envs.tetris_env import TetrisVecEnv
     out = {}
     for fmt in ("packed", "f32"):
@@ -691,8 +764,10 @@ def clear_heavy(head, cfg_kw, C, ShardedTetris, timed, roofline, kname_of, dev, 
     r = {"value": n_global * K / el, "ms_per_step": el / K * 1e3, "p_lock": pl,
          "lines_per_env_step": (n_cleared / 100.0 / (ce.n * K)) if config == "c3" else None,
          "actions": "st_policy_greedy (greedy placement, 3% uniform), recorded then replayed",
-         "roofline": roofline(kern_us, bpe, ce.n, kname_of("step", False, not cfg_kw), grid=step_grid(ce.n), extra=
-                              {"bytes_formula": "SURVEY 8(d): 182 + 184 p_lock", "p_lock": pl})}
+         "roofline": roofline(kern_us, bpe, ce.n, kname_of("step", False, not cfg_kw), grid=None, extra=
+                              {"bytes_formula": "SURVEY 8(d): 182 + 184 p_lock", "p_lock": pl,
+                               "traffic_note": "same kernel and launch shape as the headline: a PMC pass "
+                                               "cannot tell the two workloads apart"})}
     del g
     ce.close()
     return r

@@ -22,6 +22,7 @@ struct st_ctx {
     uint32_t *piece;
     int32_t *stats;
     uint32_t *mt;
+    uint32_t *act_flag;  // st_set_action_flag (caller-owned), or null
 };
 
 namespace {
@@ -75,6 +76,7 @@ st::KParams params(const st_ctx *c) {
     p.piece = c->piece;
     p.stats = c->stats;
     p.mt = c->mt;
+    p.act_flag = c->act_flag;
     return p;
 }
 
@@ -130,7 +132,7 @@ int st_create(st_ctx **out, const st_config *cfg, int device, int64_t n_envs) {
     if (e == hipSuccess) c->piece = reinterpret_cast<uint32_t *>(c->stats) + ST_STAT_PIECE * sd;
     // MT states: [stride][kMtPitch] (+ the back pad a draw window may reach)
     if (e == hipSuccess) e = hipMalloc(&c->mt, (sd * st::kMtPitch + st::kMtPadBack) * sizeof(uint32_t));
-    // per-env 4-word draw-window cache, valid only where the MT word says so
+    // diagnostic phase stamps (ST_STAMPS set: the instrumented step kernel)
     if (e == hipSuccess && getenv("ST_STAMPS"))
         e = hipMalloc(&c->stamps, (sd / st::kWave) * st::kStampWords * sizeof(uint64_t));
     if (e != hipSuccess) {
@@ -411,6 +413,24 @@ int st_check_actions(const uint8_t *d_actions, int64_t n, uint32_t *d_flag, st_s
     if (n < 0) return fail(ST_EINVAL, "st_check_actions: negative size");
     if (n > 0 && (!d_actions || !d_flag)) return fail(ST_EINVAL, "st_check_actions: null argument");
     ST_HIP(st::launch_check_actions(d_actions, n, d_flag, (hipStream_t)stream));
+    return ST_OK;
+}
+
+int st_set_action_flag(st_ctx *c, uint32_t *d_flag) {
+    if (!c) return fail(ST_EINVAL, "st_set_action_flag: null context");
+    c->act_flag = d_flag;
+    return ST_OK;
+}
+
+int st_stream_sync(st_stream stream) {
+    ST_HIP(hipStreamSynchronize((hipStream_t)stream));
+    return ST_OK;
+}
+
+int st_host_device_ptr(void *host, void **d_out) {
+    if (!host || !d_out) return fail(ST_EINVAL, "st_host_device_ptr: null argument");
+    *d_out = nullptr;
+    ST_HIP(hipHostGetDevicePointer(d_out, host, 0));
     return ST_OK;
 }
 

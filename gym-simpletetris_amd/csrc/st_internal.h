@@ -52,6 +52,7 @@ struct KParams {
     float *obs_f32;          // [n][W][H]
     int32_t *reward;         // [n]
     uint8_t *done;           // [n]
+    uint32_t *act_flag;      // st_set_action_flag: sticky "action outside 0..6" word, or null
 };
 
 hipError_t launch_seed(const KParams &p, hipStream_t s);

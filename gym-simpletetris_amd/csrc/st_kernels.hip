@@ -852,11 +852,15 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
     auto ss = [&](int r) -> uint32_t & { return SS[r * kWave + lane]; };
     auto tab = [&](int i) -> uint2 { return *reinterpret_cast<const uint2 *>(&sm.T2[2 * i]); };
 
+    // an action outside value_action_map in any step of this launch (the
+    // reference's KeyError, tetris_env.py:245; the step treats it as idle)
+    [[maybe_unused]] bool bad_act = false;
     for (int t = 0; t < K; ++t) {
     // ---------------- logic: action, gravity, lock decision ----------------
     uint32_t act = 6u;
     if constexpr (ACT) {
         act = real ? act_next : 6u;
+        bad_act |= act > 6u;
         if (KSTEPS != 1 && t + 1 < K) act_next = p.actions[(int64_t)(t + 1) * p.n + (real ? e : p.n - 1)];
     }
     uint32_t *const obs_t = p.obs ? p.obs + (int64_t)t * W * p.n : nullptr;
@@ -1376,6 +1380,12 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
     }
     }  // for t
     wave_sync();
+    if constexpr (ACT) {
+        // st_set_action_flag's sticky word: only lanes that saw a bad action
+        // store (a raw buffer store with an out-of-range offset elsewhere, no
+        // branch); a null flag has an empty range, so nothing is written
+        __builtin_amdgcn_raw_buffer_store_b32(1u, buf_rsrc(p.act_flag, 4u), bad_act ? 0u : kOff, 0, 0);
+    }
     if constexpr (KSTEPS != 1 && DO_L) {
         // 32-bit buffer offsets: 64-bit row offsets shared with the prologue
         // would stay live (in SGPRs) across the step loop

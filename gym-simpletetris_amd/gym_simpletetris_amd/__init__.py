@@ -9,20 +9,27 @@ is importable the ids are registered there too.
 """
 import os as _os
 
-# Kernel arguments in device memory for every launch: the step is one short
-# launch per env-step, and this measured 1-5% faster per step on MI355X
-# (DESIGN §5.1).  HIP reads it once, when its runtime starts, so it applies
-# when this package is imported before anything touches the GPU; an explicit
-# non-empty setting in the environment wins (HIP reads an empty one as 0).
-if not _os.environ.get("HIP_FORCE_DEV_KERNARG"):
-    _os.environ["HIP_FORCE_DEV_KERNARG"] = "1"
-
 from .engine import SHAPE_NAMES, TetrisBatch  # noqa: F401
 from .envs import TetrisEnv, TetrisVecEnv  # noqa: F401
 
 __version__ = "0.1.0"
 
 ENV_IDS = ("SimpleTetris-v0", "SimpleTetrisVec-v0")
+
+
+def tune_runtime(force_dev_kernarg: bool = True) -> bool:
+    """Opt-in HIP runtime setting for step-per-launch loops: kernel arguments
+    in device memory for every launch (HIP_FORCE_DEV_KERNARG=1), measured
+    1-5% faster per st_step on MI355X.  It applies to
+    every HIP kernel of the process (and its children) and HIP reads it only
+    when its runtime starts, so call this before anything touches the GPU;
+    an explicit non-empty setting in the environment wins.  Returns whether
+    the variable now holds the requested value.  Importing the package
+    changes nothing."""
+    want = "1" if force_dev_kernarg else "0"
+    if not _os.environ.get("HIP_FORCE_DEV_KERNARG"):
+        _os.environ["HIP_FORCE_DEV_KERNARG"] = want
+    return _os.environ["HIP_FORCE_DEV_KERNARG"] == want
 
 
 def make(env_id: str = "SimpleTetris-v0", **kwargs):

@@ -38,7 +38,8 @@ EXPORT_MT, EXPORT_OBS_F32 = 1, 2  # st_export_env parts
 
 EXPORTS = ("st_create", "st_destroy", "st_seed", "st_reset", "st_step", "st_step_f32", "st_rollout",
            "st_obs_to_f32", "st_render", "st_grayscale", "st_state", "st_copy", "st_mt_sync", "st_state_bytes", "st_save",
-           "st_load", "st_export_env", "st_export_words", "st_check_actions", "st_gen_actions", "st_policy_greedy", "st_debug_stamps", "st_last_error", "st_abi_version")
+           "st_load", "st_export_env", "st_export_words", "st_check_actions", "st_set_action_flag", "st_stream_sync",
+           "st_host_device_ptr", "st_gen_actions", "st_policy_greedy", "st_debug_stamps", "st_last_error", "st_abi_version")
 
 
 class StError(RuntimeError):
@@ -98,6 +99,9 @@ def load(path: str = LIB_PATH):
         "st_export_env": ([vp, i64, vp, vp, vp, u32, vp, vp], ctypes.c_int),
         "st_export_words": ([i32, i32], ctypes.c_int),
         "st_check_actions": ([vp, i64, vp, vp], ctypes.c_int),
+        "st_set_action_flag": ([vp, vp], ctypes.c_int),
+        "st_stream_sync": ([vp], ctypes.c_int),
+        "st_host_device_ptr": ([vp, ctypes.POINTER(vp)], ctypes.c_int),
         "st_gen_actions": ([vp, i64, i64, u64, i64, vp], ctypes.c_int),
         "st_policy_greedy": ([vp, u64, i64, ctypes.c_uint32, vp, vp], ctypes.c_int),
         "st_debug_stamps": ([vp, vp, i64], ctypes.c_int),

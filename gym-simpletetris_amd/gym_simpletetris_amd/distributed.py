@@ -96,6 +96,9 @@ class ShardedTetris:
         self.offset, self.n = shard_range(n_global, self.world, self.rank)
         self.n_cap = shard_cap(n_global, self.world)
         self.counts = [shard_range(n_global, self.world, r)[1] for r in range(self.world)]
+        # the public step stays asynchronous: actions are range-checked by the
+        # step kernel (validate_actions='async'), not by a per-step sync
+        engine_kwargs.setdefault("validate_actions", "async")
         self.engine = TetrisBatch(self.n, device=device,
                                   seeds=[seed + self.offset + e for e in range(self.n)],
                                   **engine_kwargs)
@@ -107,7 +110,9 @@ class ShardedTetris:
 
     def step(self, actions: torch.Tensor):
         """Step the shard, writing straight into the gather buffer (the
-        engine's own action checks apply: shape, dtype, device, 0..6)."""
+        engine's own action checks apply: shape, dtype, device, and 0..6 --
+        by default in the step kernel, so a KeyError for an out-of-range
+        device action comes at the next step or engine.check_actions())."""
         return self.engine.step(actions, obs="packed", out=(self._obs, self._rew, self._done))
 
     def gather(self, dst: int = 0, cpu: bool = False):

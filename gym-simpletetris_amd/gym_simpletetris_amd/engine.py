@@ -40,15 +40,40 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[ctypes.c_void_p]:
 
 
 def _mapped(t: torch.Tensor):
-    """Device address of a pinned host tensor (hipHostGetDevicePointer), or
-    None if the runtime does not map it for the device."""
-    try:
-        hip = ctypes.CDLL("libamdhip64.so")
-        dp = ctypes.c_void_p()
-        rc = hip.hipHostGetDevicePointer(ctypes.byref(dp), ctypes.c_void_p(t.data_ptr()), 0)
-        return dp if rc == 0 and dp.value else None
-    except OSError:
-        return None
+    """Device address of a pinned host tensor (st_host_device_ptr, i.e.
+    hipHostGetDevicePointer in the runtime the kernels use), or None if the
+    runtime does not map it for the device."""
+    L = C.load()
+    dp = ctypes.c_void_p()
+    rc = L.st_host_device_ptr(ctypes.c_void_p(t.data_ptr()), ctypes.byref(dp))
+    return dp if rc == 0 and dp.value else None
+
+
+def scalar_action(a) -> int:
+    """value_action_map[a] (tetris_env.py:152-160, :245) for one action: ints,
+    bools and numpy integers index by value; a float finds a key only when it
+    equals one (2.0 -> 2, as in a dict lookup); anything else raises KeyError."""
+    if isinstance(a, (bool, np.bool_, int, np.integer)):
+        v = int(a)
+    elif isinstance(a, (float, np.floating)) and float(a).is_integer():
+        v = int(a)
+    else:
+        raise KeyError(a)
+    if not 0 <= v < 7:
+        raise KeyError(a)
+    return v
+
+
+def _bad_actions(x: torch.Tensor) -> torch.Tensor:
+    """Elementwise "not a key of value_action_map" for an action tensor (the
+    same rule as scalar_action: floats must be integral)."""
+    if x.dtype == torch.bool:
+        return torch.zeros_like(x)
+    if x.dtype.is_floating_point:
+        return ~((x >= 0) & (x <= 6) & (x == torch.floor(x)))
+    if x.dtype == torch.uint8:
+        return x > 6
+    return (x < 0) | (x > 6)
 
 
 def _from_dlpack(x):
@@ -104,24 +129,28 @@ class TetrisBatch:
         # value_action_map[action] KeyError (tetris_env.py:245).  For a device
         # tensor that check costs one device->host sync per call;
         # validate_actions=False skips it (values >= 7 then act as idle), and
-        # 'async' checks on the device (st_check_actions into a sticky flag in
-        # mapped host memory) without a sync: the KeyError comes at the next
-        # step()/rollout() after the flag is seen, or from check_actions().
+        # 'async' lets the step kernel check the actions it loads anyway (a
+        # sticky flag in mapped host memory, st_set_action_flag) without a
+        # sync: the KeyError comes at the next step()/rollout() after the flag
+        # is seen, or from check_actions().
         if validate_actions not in (True, False, "async"):
             raise ValueError("validate_actions must be True, False or 'async'")
         self.validate_actions = validate_actions
         self._flag_h = self._flag_dev = None
-        if validate_actions == "async":
-            self._flag_h = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-            self._flag_np = self._flag_h.numpy()
-            self._flag_dev = _mapped(self._flag_h)
-            if self._flag_dev is None:
-                raise RuntimeError("validate_actions='async' needs pinned host memory mapped for the device")
         cfg = C.Config(self.width, self.height, self.lock_delay, flags, C.AUTORESET[autoreset])
         ctx = ctypes.c_void_p()
         with torch.cuda.device(device):
             C.check(self._L.st_create(ctypes.byref(ctx), ctypes.byref(cfg), device.index, self.n))
         self._ctx = ctx
+        if validate_actions == "async":
+            # the step kernels' own action check (st_set_action_flag) into a
+            # sticky word of pinned host memory mapped for the device
+            self._flag_h = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._flag_np = self._flag_h.numpy()
+            self._flag_dev = _mapped(self._flag_h)
+            if self._flag_dev is None:
+                raise RuntimeError("validate_actions='async' needs pinned host memory mapped for the device")
+            C.check(self._L.st_set_action_flag(ctx, self._flag_dev))
         v = C.StateViews()
         C.check(self._L.st_state(ctx, ctypes.byref(v)))
         self._views = v
@@ -178,38 +207,51 @@ class TetrisBatch:
         return t.contiguous()
 
     def _actions(self, x, lead=()) -> torch.Tensor:
-        """Actions as a contiguous uint8 device tensor of shape lead + (n,),
-        range-checked BEFORE the cast (a cast would wrap -1 to 255 and 263 to
-        7): the reference raises KeyError for an action outside
-        value_action_map (tetris_env.py:152-160, :245)."""
+        """Actions as a contiguous uint8 device tensor of shape lead + (n,).
+        The reference raises KeyError for an action outside value_action_map
+        (tetris_env.py:152-160, :245); a uint8 cast would wrap -1 to 255 and
+        263 to 7, so values are checked BEFORE it:
+          validate_actions=True: on the host, immediately (for a device tensor
+            one device->host sync);
+          'async': by the step kernel itself (st_set_action_flag: the kernel
+            sets a sticky word in mapped host memory when an action is > 6,
+            polled here without a sync); non-uint8 tensors get their bad values
+            mapped to 255 on the device first, so the kernel sees them;
+          False: no check (values > 6 act as idle)."""
         shape = tuple(lead) + (self.n,)
+        asyn = self.validate_actions == "async"
+        if asyn:
+            self._raise_flagged()
         if (self.validate_actions is not True and type(x) is torch.Tensor and x.dtype == torch.uint8
                 and x.device == self.device and x.is_contiguous() and tuple(x.shape) == shape):
-            if self.validate_actions == "async":  # an RL loop's own device buffer, checked on the GPU
-                self._raise_flagged()
-                C.check(self._L.st_check_actions(_ptr(x), x.numel(), self._flag_dev, self._stream()))
-            return x
+            return x  # an RL loop's own device buffer: checked in the step kernel ('async') or not at all
         x = _from_dlpack(x)
         if isinstance(x, torch.Tensor):
-            if x.dtype.is_floating_point or x.dtype == torch.bool or x.is_complex():
-                raise TypeError(f"actions must be integers, got {x.dtype}")
+            if x.is_complex():
+                raise TypeError(f"actions must be real numbers, got {x.dtype}")
             if tuple(x.shape) != shape and x.numel() != int(np.prod(shape)):
                 raise ValueError(f"actions must have shape {shape}, got {tuple(x.shape)}")
-            if self.validate_actions or x.device != self.device:
-                bad = (x < 0) | (x > 6) if x.dtype != torch.uint8 else (x > 6)
+            if self.validate_actions is True or x.device != self.device:
+                bad = _bad_actions(x)
                 if bool(bad.any()):
                     v = x[bad].flatten()[0].item()
                     raise KeyError(f"action {v} not in 0..6 (tetris_env.py:245)")
+            elif asyn and x.dtype != torch.uint8:  # keep bad values visible to the kernel's check
+                x = torch.where(_bad_actions(x), torch.full_like(x, 255), x)
             t = x if (x.dtype == torch.uint8 and x.device == self.device) \
-                else x.to(device=self.device, dtype=torch.uint8)
+                else x.to(device=self.device).to(torch.uint8)
             return t.reshape(shape).contiguous()
         a = np.asarray(x)
-        if a.dtype.kind not in "iub":
-            a = a.astype(np.int64)
         if a.size != int(np.prod(shape)):
             raise ValueError(f"actions must have shape {shape}, got {a.shape}")
-        if a.size and (int(a.min()) < 0 or int(a.max()) > 6):
-            v = a.flat[np.flatnonzero((a < 0) | (a > 6))[0]]
+        if a.dtype.kind == "f":
+            ok = (a >= 0) & (a <= 6) & (a == np.floor(a))
+        elif a.dtype.kind in "iub":
+            ok = (a >= 0) & (a <= 6)
+        else:
+            raise TypeError(f"actions must be numbers, got {a.dtype}")
+        if a.size and not ok.all():
+            v = a.flat[np.flatnonzero(~ok)[0]]
             raise KeyError(f"action {v} not in 0..6 (tetris_env.py:245)")
         return torch.as_tensor(a.astype(np.uint8).reshape(shape), device=self.device)
 

@@ -27,7 +27,7 @@ import torch
 
 from .. import _lib as C
 from .. import spaces
-from ..engine import SHAPE_NAMES, TetrisBatch, _mapped
+from ..engine import SHAPE_NAMES, TetrisBatch, _mapped, scalar_action
 
 
 # counter rows of the export record (st_stat)
@@ -48,23 +48,15 @@ def _obs_space(obs_type, width, height, extend_dims):
     return spaces.Box(0, 1, shape=shape, dtype=np.float32)
 
 
-def _stream_sync(sp: ctypes.c_void_p, device):
-    """A synchronize of stream `sp`: hipStreamSynchronize through ctypes, or
-    torch's where the HIP runtime library cannot be opened by name."""
-    try:
-        hip = ctypes.CDLL("libamdhip64.so")
-        fn = hip.hipStreamSynchronize
-        fn.argtypes = [ctypes.c_void_p]
-        fn.restype = ctypes.c_int
+def _stream_sync(sp: ctypes.c_void_p):
+    """A synchronize of stream `sp` through libsimpletetris (st_stream_sync:
+    the runtime its kernels use; torch's stream synchronize costs ~3 us more
+    per call)."""
+    fn = C.load().st_stream_sync
 
-        def sync():
-            rc = fn(sp)
-            if rc != 0:
-                raise RuntimeError(f"hipStreamSynchronize failed ({rc})")
-        return sync
-    except (OSError, AttributeError):
-        stream = torch.cuda.current_stream(device)
-        return stream.synchronize
+    def sync():
+        C.check(fn(sp))
+    return sync
 
 
 class TetrisEnv:
@@ -138,7 +130,7 @@ class TetrisEnv:
                                         for t in (self.engine.obs, self.engine.reward, self.engine.done))
         self._pz = ctypes.c_void_p(self._zeros.data_ptr())
         self._sp = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-        self._sync = _stream_sync(self._sp, dev)
+        self._sync = _stream_sync(self._sp)
 
     # ------------------------------------------------------------- RNG mirror
     def seed(self, seed=None):
@@ -260,13 +252,11 @@ class TetrisEnv:
         """TetrisEnv.step (tetris_env.py:397-403)."""
         if not self._started:
             raise AttributeError("step() before reset(): the reference fails at tetris_env.py:244")
-        if isinstance(action, (bool, np.bool_)) or not isinstance(action, (int, np.integer)) \
-                or not 0 <= int(action) < 7:
-            raise KeyError(action)  # value_action_map[action], tetris_env.py:245
+        action = scalar_action(action)  # value_action_map[action]'s KeyError, tetris_env.py:245
         prev = self._stats
         self._push_rng()
         eng = self.engine
-        C.check(eng._L.st_step(eng._ctx, self._p_acts[int(action)], self._po, self._pr, self._pd, self._sp))
+        C.check(eng._L.st_step(eng._ctx, self._p_acts[action], self._po, self._pr, self._pd, self._sp))
         obs, r, d, st, img = self._readback(self._po, self._pr, self._pd, prev[C.STAT["mt_index"]])
         self._stats = st
         return self._observation(obs, img), self._typed_reward(r, d, prev, st), d, self._get_info(st)
@@ -338,11 +328,14 @@ class TetrisVecEnv:
     terminal observation (what the reference's step returned) and
     info['ep_score'] / ['ep_lines'] / ['ep_time'] / ['ep_holes'] hold the
     finished episode's counters.  Buffers are reused between steps.
-    Actions outside 0..6 raise KeyError like the reference's; for actions
-    already on the GPU that check is one device->host sync per step, which
-    `validate_actions=False` removes (the loop then stays asynchronous;
-    out-of-range values act as idle) and `validate_actions='async'` moves to
-    the GPU (the KeyError then comes at a later step or check_actions()).
+    Actions outside 0..6 raise KeyError like the reference's.  By default
+    (`validate_actions='async'`) the step kernel checks the actions it loads
+    anyway and sets a sticky flag in mapped host memory: no extra launch and
+    no sync, the KeyError comes at the next step() after the flag is seen or
+    from check_actions().  `validate_actions=True` checks before the step
+    (the reference's immediate KeyError; for actions already on the GPU one
+    device->host sync per step); `False` does not check (out-of-range values
+    act as idle).  Host (numpy / list) actions are always checked up front.
     """
 
     def __init__(self, num_envs: int, width=10, height=20, obs_type="ram", extend_dims=False,
@@ -350,7 +343,7 @@ class TetrisVecEnv:
                  advanced_clears=False, high_scoring=False, penalise_holes=False,
                  penalise_holes_increase=False, lock_delay=0, step_reset=False, *,
                  device=None, seed: int = 0, global_offset: int = 0, autoreset: bool = True,
-                 obs_format: str = "f32", validate_actions: bool = True):
+                 obs_format: str = "f32", validate_actions="async"):
         if obs_format not in ("f32", "packed"):
             raise ValueError("obs_format must be 'f32' or 'packed'")
         self.num_envs = int(num_envs)

@@ -251,11 +251,29 @@ int st_gen_actions(uint8_t *d_out, int64_t n, int64_t t, uint64_t seed,
                    int64_t global_offset, st_stream stream);
 
 /* Sticky check for actions outside 0..6 (the reference raises KeyError for
- * them, tetris_env.py:245; st_step treats them as idle): sets *d_flag = 1 if
+ * them, tetris_env.py:245; st_step treats them as idle) as its own launch,
+ * for an action batch not (yet) passed to a step: sets *d_flag = 1 if
  * any of d_actions[0..n) is > 6, never clears it.  d_flag may be host memory
  * mapped for the device, so the caller can poll it without synchronising
  * (the batched surface's validate_actions='async'). */
 int st_check_actions(const uint8_t *d_actions, int64_t n, uint32_t *d_flag, st_stream stream);
+
+/* The same check fused into the step kernels: once a flag word is set,
+ * every st_step / st_step_f32 / st_rollout on this context sets *d_flag = 1
+ * when any of its actions is > 6 (never clears it), from the action loads the
+ * step does anyway -- no extra launch, no sync.  d_flag: device memory or host
+ * memory mapped for the device (st_host_device_ptr), owned by the caller and
+ * valid until it is replaced; NULL turns the check off (the default). */
+int st_set_action_flag(st_ctx *ctx, uint32_t *d_flag);
+
+/* Runtime helpers for hosts that bind only this library (the Python package
+ * uses them instead of opening the HIP runtime by name, which could load a
+ * second runtime copy beside the one the kernels use):
+ * st_stream_sync: hipStreamSynchronize(stream);
+ * st_host_device_ptr: the device address of pinned, mapped host memory
+ * (hipHostGetDevicePointer). */
+int st_stream_sync(st_stream stream);
+int st_host_device_ptr(void *host, void **d_out);
 
 /* Diagnostics: when the environment variable ST_STAMPS is set at st_create,
  * st_step runs an instrumented build of the step kernel that records

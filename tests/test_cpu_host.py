@@ -66,6 +66,35 @@ def test_make_ids():
         G.make("SimpleTetris-v1")
 
 
+def test_scalar_action_follows_the_reference_dict():
+    """value_action_map[a] (tetris_env.py:152-160, :245): the keys are the
+    ints 0..6; equal numbers of other types hit them (True, 2.0, np.int8),
+    anything else raises KeyError."""
+    from gym_simpletetris_amd.engine import scalar_action
+    ref = {i: i for i in range(7)}
+    for a in (0, 6, 2.0, np.float32(5.0), np.int64(3), np.uint8(1), True, False):
+        assert scalar_action(a) == ref[a]
+    for a in (7, -1, 2.5, float("nan"), float("inf"), "2", None, np.float64(6.5)):
+        with pytest.raises(KeyError):
+            scalar_action(a)
+        with pytest.raises((KeyError, TypeError)):
+            ref[a]
+
+
+def test_import_leaves_hip_environment_alone():
+    """Importing the package changes no process-wide HIP setting;
+    tune_runtime() is the explicit opt-in."""
+    import subprocess
+    import sys
+    code = ("import os, sys; sys.path.insert(0, 'gym-simpletetris_amd'); "
+            "os.environ.pop('HIP_FORCE_DEV_KERNARG', None); import gym_simpletetris_amd as G; "
+            "assert 'HIP_FORCE_DEV_KERNARG' not in os.environ; "
+            "assert G.tune_runtime() and os.environ['HIP_FORCE_DEV_KERNARG'] == '1'; print('ok')")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", out.stderr[-2000:]
+
+
 def test_spaces_stand_ins():
     from gym_simpletetris_amd import spaces
     d = spaces.Discrete(7)
@@ -166,34 +195,69 @@ def test_algorithmic_bytes_formula():
     assert bench.algorithmic_bytes(10, 20, 1.0, False) > b
 
 
-def test_bench_roofline_bytes_and_pmc_tie():
+def test_bench_roofline_bytes_and_pmc_tie(tmp_path, monkeypatch):
+    """bench.py prices a launch with PMC traffic / rocprof durations only
+    from a summary of the same kernel sources AND the same launch shape
+    (kernel, grid, steps per launch); the summary tools key them so."""
     import json
+    import sys
     import bench
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import pmc_summary
     assert bench.s8d_bytes(0.0, False) == 182 and bench.s8d_bytes(1.0, False) == 366
     assert bench.s8d_bytes(0.5, True) == 902 + 92
     assert abs(bench.algorithmic_bytes(10, 20, 1.0, False) - (102 + 167.7)) < 1e-9
-    # traffic is taken only from a PMC summary of the same kernel sources
-    pmc = os.path.join(ROOT, "profiles", "r02_pmc.json")
-    d = json.load(open(pmc))
-    kname = "k_step<10, 20, false, false, true>@%d" % bench.step_grid(65536)
-    got, src = bench.load_pmc(kname, d["kernel_source_sha"])
-    assert src == "r02_pmc.json" and got == d["kernels"][kname]["hbm_bytes_per_launch"]
     assert bench.step_grid(4096) == 8192 and bench.step_grid(65536) == 131072
-    got, why = bench.load_pmc(kname, "0" * 16)
-    assert got is None and "no PMC pass" in why
     assert len(bench.kernel_source_sha()) == 16
-    # the rocprofv3 trace stats come the same way, from a trace of the same sources
-    tj = json.load(open(os.path.join(ROOT, "profiles", "r02_trace.json")))
-    tr = bench.load_trace(kname, tj["kernel_source_sha"])
-    assert tr["launches"] == tj["kernels"][kname]["launches"] and tr["source"] == "r02_trace.json"
-    assert bench.load_trace(kname, "0" * 16) is None
-    # the image kernels' launch keys as bench.py derives them are the ones the
-    # PMC pass recorded (launch_grayscale's choice of kernel and grid)
+    step = bench.launch_key("k_step<10, 20, false, false, true>", bench.step_grid(65536), 1)
+    ro = bench.launch_key("k_rollout<10, 20, false, true>", bench.step_grid(65536), 100)
+    assert step.endswith("@131072@k1") and ro.endswith("@131072@k100")
+    assert pmc_summary.launch_k("void st::(anonymous namespace)::k_rollout<10, 20, false, true>(st::KParams)", 100) == 100
+    assert pmc_summary.launch_k("void st::(anonymous namespace)::k_step<10, 20, false, false, true>(st::KParams)", 100) == 1
+    sha = bench.kernel_source_sha()
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    (prof / "rX_pmc.json").write_text(json.dumps({"kernel_source_sha": sha, "kernels": {
+        step: {"hbm_bytes_per_launch": 1.5e7}, ro: {"hbm_bytes_per_launch": 3e8}}}))
+    (prof / "rX_trace.json").write_text(json.dumps({"kernel_source_sha": sha, "kernels": {
+        step: {"mean_us": 5.0, "median_us": 4.9, "launches": 4000, "trace": "t.csv", "p_lock": 0.2}}}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    got, src = bench.load_pmc(step, sha)
+    assert got == 1.5e7 and src == "rX_pmc.json"
+    assert bench.load_pmc(ro, sha)[0] == 3e8
+    # another launch shape (a 20-step rollout) or other sources: no number
+    got, why = bench.load_pmc(ro.replace("@k100", "@k20"), sha)
+    assert got is None and "launch shape" in why
+    assert bench.load_pmc(step, "0" * 16)[0] is None
+    tr = bench.load_trace(step, sha)
+    assert tr["launches"] == 4000 and tr["p_lock"] == 0.2 and tr["source"] == "rX_trace.json"
+    assert bench.load_trace(step, "0" * 16) is None
+    # p_lock per launch key from a bench JSON line's roofline objects
+    bj = tmp_path / "b.json"
+    bj.write_text("noise\n" + json.dumps({"roofline": {"launch_key": step, "p_lock": 0.21},
+                                          "variants": {"rollout_packed": {"roofline": {"launch_key": ro, "p_lock": 0.2}},
+                                                       "note": "x"}}))
+    assert pmc_summary.bench_p_lock(str(bj)) == {step: 0.21, ro: 0.2}
+    # the image kernels' launch keys as bench.py derives them
     for ch in (1, 3):
-        key = "%s@%d" % bench.image_launch(65536, 84, ch, False)
-        assert key in d["kernels"], key
-    # the committed profiles describe the committed kernel sources
+        name, grid = bench.image_launch(65536, 84, ch, False)
+        assert name.startswith("k_grayscale") and grid > 0
+
+
+def test_committed_profiles_match_sources():
+    """The newest committed PMC and trace summaries describe the committed
+    kernel sources (so the bench line's traffic / rocprof are not null) and
+    carry launch-shape keys."""
+    import glob
+    import json
+    import bench
+    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+    trs = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_trace.json")))
+    d, tj = json.load(open(pmcs[-1])), json.load(open(trs[-1]))
     assert d["kernel_source_sha"] == tj["kernel_source_sha"] == bench.kernel_source_sha()
+    head = bench.launch_key("k_step<10, 20, false, false, true>", bench.step_grid(65536), 1)
+    assert head in d["kernels"] and head in tj["kernels"]
+    assert tj["kernels"][head]["p_lock"] is not None
 
 
 def test_bench_cpu_baseline_all_cores():

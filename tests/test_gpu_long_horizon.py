@@ -120,7 +120,11 @@ def _compare(t0, got_r, got_d, got_o, ref):
 
 @pytest.mark.parametrize("config,launch", [("c3", "eager"), ("c3", "graph"), ("c4", "eager")])
 def test_bench_workload_st_step(config, launch):
-    """bench.py's headline region (eager: the default; graph: `--launch graph`)."""
+    """bench.py's headline region (eager: the default; graph: `--launch
+    graph`, K launches captured in one hipGraph and replayed).  In the graph
+    case the outputs of the timed steps hold a sentinel after the capture
+    (capturing runs nothing) and the oracle's values after the replay: the
+    compared steps really came from the graph."""
     import gym_simpletetris_amd as G
     from gym_simpletetris_amd import _lib as C
     dev = torch.device("cuda", 0)
@@ -132,35 +136,41 @@ def test_bench_workload_st_step(config, launch):
     for t in range(T):
         eng.gen_actions(t, ASEED, out=acts[t])
     eng.reset()
-    obs = torch.empty((T, W, N), dtype=torch.int32, device=dev)
-    rew = torch.empty((T, N), dtype=torch.int32, device=dev)
-    done = torch.empty((T, N), dtype=torch.uint8, device=dev)
+    SENT = -12345
+    obs = torch.full((T, W, N), SENT, dtype=torch.int32, device=dev)
+    rew = torch.full((T, N), SENT, dtype=torch.int32, device=dev)
+    done = torch.full((T, N), 7, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize(dev)
     L, ctx = eng._L, eng._ctx
     s = torch.cuda.Stream(dev)
     sp = ctypes.c_void_p(s.cuda_stream)
 
-    def launch(t):
+    def launch_step(t):
         C.check(L.st_step(ctx, ctypes.c_void_p(acts[t].data_ptr()), ctypes.c_void_p(obs[t].data_ptr()),
                           ctypes.c_void_p(rew[t].data_ptr()), ctypes.c_void_p(done[t].data_ptr()), sp))
     with torch.cuda.stream(s):
         for t in range(WU):  # bench warm-up: eager launches
-            launch(t)
+            launch_step(t)
     torch.cuda.synchronize(dev)
     if launch == "graph":
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=s):  # bench --launch graph: one graph of K launches
             for t in range(WU, T):
-                launch(t)
+                launch_step(t)
+        torch.cuda.synchronize(dev)
+        # captured, not run: every timed step's outputs still hold the sentinel
+        assert bool((rew[WU:] == SENT).all()) and bool((obs[WU:] == SENT).all()) and bool((done[WU:] == 7).all())
         with torch.cuda.stream(s):
             g.replay()
         torch.cuda.synchronize(dev)
         del g
     else:
+        assert launch == "eager"
         with torch.cuda.stream(s):  # bench default: K eager launches
             for t in range(WU, T):
-                launch(t)
+                launch_step(t)
         torch.cuda.synchronize(dev)
+    assert not bool((rew == SENT).any()) and not bool((done == 7).any())
     orc = ParallelOracle(N, kw)
     try:
         CH = 100
@@ -173,6 +183,45 @@ def test_bench_workload_st_step(config, launch):
         fin = orc.final_state()["rng"]["mt"].astype(np.uint32)
         gen1 = _twist_np(_seeded_words(N))
         assert (fin != gen1).any(axis=1).mean() > 0.5
+    finally:
+        orc.close()
+        eng.close()
+
+
+def test_c2_shape_eager_long():
+    """BASELINE C2 at its own shape: 4,096 10x20 boards, C3 (default)
+    rewards, same-step auto-reset, 1,200 eager st_step launches (one per
+    step, as bench.py times C2), every step's reward / done / packed obs and
+    the final state bit-exact against the oracle."""
+    import gym_simpletetris_amd as G
+    from gym_simpletetris_amd import _lib as C
+    n, T = 4096, 1200
+    dev = torch.device("cuda", 0)
+    eng = G.TetrisBatch(n, autoreset="same_step", seeds=[SEED_BASE + e for e in range(n)],
+                        device=dev, width=W, height=H)
+    acts = torch.empty((T, n), dtype=torch.uint8, device=dev)
+    for t in range(T):
+        eng.gen_actions(t, ASEED, out=acts[t])
+    eng.reset()
+    obs = torch.empty((T, W, n), dtype=torch.int32, device=dev)
+    rew = torch.empty((T, n), dtype=torch.int32, device=dev)
+    done = torch.empty((T, n), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+    L, ctx = eng._L, eng._ctx
+    sp = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    for t in range(T):
+        C.check(L.st_step(ctx, ctypes.c_void_p(acts[t].data_ptr()), ctypes.c_void_p(obs[t].data_ptr()),
+                          ctypes.c_void_p(rew[t].data_ptr()), ctypes.c_void_p(done[t].data_ptr()), sp))
+    torch.cuda.synchronize(dev)
+    orc = ParallelOracle(n, {})
+    try:
+        CH = 200
+        for t0 in range(0, T, CH):
+            ref = orc.rollout(t0, CH)
+            _compare(t0, rew[t0:t0 + CH].cpu().numpy(), done[t0:t0 + CH].cpu().numpy(),
+                     obs[t0:t0 + CH].cpu().numpy().view(np.uint32), ref)
+        _check_final(eng, orc)
+        assert int(done.sum()) > n  # episodes turned over inside the compared span
     finally:
         orc.close()
         eng.close()

@@ -459,6 +459,12 @@ def test_single_env_errors_and_render():
     env.reset()
     with pytest.raises(KeyError):
         env.step(7)
+    for bad in (2.5, -1, float("nan"), "2", None):  # not keys of value_action_map
+        with pytest.raises(KeyError):
+            env.step(bad)
+    env.step(2.0)  # value_action_map[2.0] is value_action_map[2]
+    env.step(np.int8(3))
+    env.step(True)  # True == 1 and hashes alike: right
     img = env.render("rgb_array")
     assert img.shape == (160, 160, 3) and img.dtype == np.uint8
     assert set(np.unique(img)) <= {0, 128, 190} and (img == 190).any()  # piece drawn
@@ -534,29 +540,47 @@ def test_vec_env_surface():
 
 def test_vec_env_unvalidated_actions():
     """validate_actions=False: no check (no sync); an out-of-range action acts
-    as idle (action 6), in-range ones as usual; the default raises KeyError."""
+    as idle (action 6), in-range ones as usual.  The default ('async': the
+    step kernel's own check) raises KeyError at the next step; True raises
+    before the step."""
     G = _engine()
     n = 512
     a = G.TetrisVecEnv(n, seed=4, validate_actions=False, obs_format="packed")
     b = G.TetrisVecEnv(n, seed=4, obs_format="packed")
+    c = G.TetrisVecEnv(n, seed=4, obs_format="packed", validate_actions=True)
+    assert b.engine.validate_actions == "async"
     a.reset()
     b.reset()
+    c.reset()
     g = torch.Generator(device="cpu").manual_seed(0)
     for t in range(60):
         acts = torch.randint(0, 10, (n,), dtype=torch.uint8, generator=g).to(a.device)
         oa, ra, da, _ = a.step(acts)
-        ob, rb, db, _ = b.step(torch.where(acts > 6, torch.full_like(acts, 6), acts))
+        ok = torch.where(acts > 6, torch.full_like(acts, 6), acts)
+        ob, rb, db, _ = b.step(ok)
+        oc, rc, dc, _ = c.step(ok)
         assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
+        assert torch.equal(oa, oc) and torch.equal(ra, rc) and torch.equal(da, dc), t
+    b.check_actions()  # nothing flagged
+    b.step(torch.full((n,), 7, dtype=torch.uint8, device=b.device))  # flagged by the kernel, no sync
     with pytest.raises(KeyError):
-        b.step(torch.full((n,), 7, dtype=torch.uint8, device=b.device))
+        b.check_actions()
+    with pytest.raises(KeyError):
+        c.step(torch.full((n,), 7, dtype=torch.uint8, device=c.device))
+    for v in (a, b, c):
+        v.close()
 
 
 def test_async_action_check():
-    """validate_actions='async': st_check_actions flags an out-of-range
-    action on the GPU without a sync; the KeyError comes at the next step
-    after the flag is seen (or from check_actions()), and the steps equal
-    unvalidated ones.  st_check_actions itself: every byte position, the
-    unaligned / ragged tail path, values 7 and 255."""
+    """validate_actions='async': the step kernel flags an out-of-range
+    action (st_set_action_flag) without a sync or an extra launch; the
+    KeyError comes at the next step after the flag is seen (or from
+    check_actions()), and the steps equal unvalidated ones.  The same for
+    st_rollout (a bad action in any of its steps), and for non-uint8 device
+    tensors (int64 -1 / 263 / 256 and non-integral floats, which a uint8
+    cast would wrap into range, are mapped to 255 on the device first).
+    st_check_actions (the stand-alone check) itself: every byte position,
+    the unaligned / ragged tail path, values 7 and 255."""
     G = _engine()
     from gym_simpletetris_amd import _lib as C
     n = 1000
@@ -581,6 +605,26 @@ def test_async_action_check():
     a.step(bad)
     with pytest.raises(KeyError):
         a.check_actions()
+    # no sync on the async path: the kernel's flag is the only check
+    assert a._flag_dev is not None
+    # st_rollout: a bad action in a later step of the launch is flagged
+    ra = torch.stack([b.gen_actions(200 + t, 3).clone() for t in range(5)])
+    a.rollout(ra)
+    a.check_actions()
+    ra[3, 999] = 7
+    a.rollout(ra)
+    with pytest.raises(KeyError):
+        a.check_actions()
+    # wider dtypes: values a uint8 cast would wrap into 0..6
+    for badv, dt in ((256, torch.int64), (-1, torch.int64), (263, torch.int32), (2.5, torch.float32)):
+        x = b.gen_actions(300, 3).to(dt)
+        x[5] = badv
+        a.step(x)
+        with pytest.raises(KeyError):
+            a.check_actions()
+    x = b.gen_actions(301, 3).to(torch.float64)  # integral floats are keys (2.0 == 2)
+    a.step(x)
+    a.check_actions()
     # the kernel on its own
     L = a._L
     sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -1010,18 +1054,31 @@ def test_wrapper_validation():
         b.step(torch.full((10,), 7, dtype=torch.uint8, device=b.device))
     with pytest.raises(KeyError):
         b.rollout(torch.full((3, 10), -1, dtype=torch.int64, device=b.device))
+    # floats index value_action_map only when integral (2.0 == 2; 2.5 is no key),
+    # on the numpy and the tensor path alike
+    for bad in (np.full(10, 2.5), np.full(10, np.nan)):
+        with pytest.raises(KeyError):
+            b.step(bad)
+        with pytest.raises(KeyError):
+            b.step(torch.as_tensor(bad, device=b.device))
     with pytest.raises(TypeError):
-        b.step(torch.zeros(10, dtype=torch.float32, device=b.device))
+        b.step(torch.zeros(10, dtype=torch.complex64, device=b.device))
     before = b.get_state()
     after = b.get_state()
     for k in before:  # rejected calls did not step
         assert np.array_equal(before[k], after[k])
     b.step(torch.arange(10, device=b.device) % 7)     # int64 device actions in range
+    b.step(np.full(10, 2.0))                         # integral floats in range
+    b.step(torch.full((10,), 3.0, device=b.device))
     from gym_simpletetris_amd.distributed import ShardedTetris
     sh = ShardedTetris(20, seed=5, rank=1, world=2, device=b.device)
+    assert sh.engine.validate_actions == "async"  # the public step stays asynchronous
     sh.reset()
+    sh.step(torch.full((10,), 9, dtype=torch.uint8, device=b.device))  # checked in the kernel
     with pytest.raises(KeyError):
-        sh.step(torch.full((10,), 9, dtype=torch.uint8, device=b.device))
+        sh.engine.check_actions()
+    with pytest.raises(KeyError):
+        sh.step(np.full(10, 9))  # host actions: checked up front
     with pytest.raises(ValueError):
         sh.step(torch.zeros(11, dtype=torch.uint8, device=b.device))
     o, r, d = sh.step(torch.zeros(10, dtype=torch.uint8, device=b.device))

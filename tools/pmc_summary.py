@@ -9,6 +9,13 @@ factors are measured on tools/pmc_calib.hip's 512 MiB streams with the step
 kernel's own 4 B/lane shapes (factor = true bytes / (counter * 1024)).
 
 usage: pmc_summary.py TAG FETCH_DIR WRITE_DIR CALIB_FETCH_DIR CALIB_WRITE_DIR
+                      [--rollout-k K] [--bench-json PATH]
+
+Entries are keyed like bench.launch_key: `name@grid@kK` (K = steps per
+launch: the pass's --rollout-chunk for k_rollout, 1 for every other kernel),
+so bench.py never prices a launch with counters of another launch shape;
+--bench-json (the JSON line of the profiled bench run) adds each key's
+p_lock from that run.
 
 The summary carries bench.kernel_source_sha() of the sources it measured;
 bench.py reports `traffic` only from a summary with its own sources' hash.
@@ -43,8 +50,38 @@ def short(name):
     return name.split("(")[0].strip()
 
 
+def launch_k(name, rollout_k):
+    """Steps per launch of a profiled kernel (bench.launch_key's k)."""
+    return rollout_k if short(name).startswith("k_rollout") else 1
+
+
+def bench_p_lock(path):
+    """launch_key -> p_lock from every roofline object of a bench JSON line."""
+    if not path:
+        return {}
+    d = json.loads(open(path).read().strip().splitlines()[-1])
+    out = {}
+    objs = [d.get("roofline", {})] + [v.get("roofline", {}) for v in d.get("variants", {}).values()
+                                       if isinstance(v, dict)]
+    for r in objs:
+        if r.get("launch_key") and r.get("p_lock") is not None:
+            out[r["launch_key"]] = r["p_lock"]
+    return out
+
+
 def main():
-    tag, fdir, wdir, cfdir, cwdir = sys.argv[1:6]
+    args = sys.argv[1:]
+    rollout_k, bench_json = 100, None
+    if "--rollout-k" in args:
+        i = args.index("--rollout-k")
+        rollout_k = int(args[i + 1])
+        del args[i:i + 2]
+    if "--bench-json" in args:
+        i = args.index("--bench-json")
+        bench_json = args[i + 1]
+        del args[i:i + 2]
+    tag, fdir, wdir, cfdir, cwdir = args[:5]
+    pl = bench_p_lock(bench_json)
     cf = per_kernel(cfdir, "FETCH_SIZE")
     cw = per_kernel(cwdir, "WRITE_SIZE")
 
@@ -62,7 +99,7 @@ def main():
     write = per_kernel(wdir, "WRITE_SIZE", by_grid=True)
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
-    out = {"tag": tag, "kernel_source_sha": bench.kernel_source_sha(),
+    out = {"tag": tag, "kernel_source_sha": bench.kernel_source_sha(), "rollout_k": rollout_k,
            "calibration": {"fetch_factor_4B_lane": f_rd4, "fetch_factor_16B_lane": f_rd16,
                            "write_factor_4B_lane": f_wr4, "raw_kib": {"rd4": raw_rd4, "rd16": raw_rd16,
                                                                      "wr4": raw_wr4},
@@ -82,12 +119,11 @@ def main():
         ent = {"launches": len(fv), "grid_size": grid, "fetch_kib": fk, "write_kib": wk,
                "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
                "hbm_bytes_per_launch": rd + wr, "full_name": name}
-        # the largest grid of a kernel (the 65,536-env workloads) under its
-        # short name (bench.load_pmc's key), every grid under name@grid
-        prev = out["kernels"].get(short(name))
-        if prev is None or grid > prev["grid_size"]:
-            out["kernels"][short(name)] = ent
-        out["kernels"][f"{short(name)}@{grid}"] = ent
+        key = f"{short(name)}@{grid}@k{launch_k(name, rollout_k)}"
+        ent["steps_per_launch"] = launch_k(name, rollout_k)
+        if key in pl:
+            ent["p_lock_profiled_run"] = pl[key]
+        out["kernels"][key] = ent
     os.makedirs("profiles", exist_ok=True)
     path = os.path.join("profiles", f"{tag}_pmc.json")
     json.dump(out, open(path, "w"), indent=1)

@@ -1,9 +1,12 @@
 """Per-kernel duration distribution from a rocprofv3 kernel trace (csv).
 
 usage: python tools/trace_summary.py <..._kernel_trace.csv> [min_run]
-       python tools/trace_summary.py --json TAG <..._kernel_trace.csv>...
-         -> JSON on stdout: per engine kernel@grid, the longest run's traced
-            duration stats, with bench.kernel_source_sha() of the sources
+       python tools/trace_summary.py --json TAG [--rollout-k K] <trace.csv[:bench.json]>...
+         -> JSON on stdout: per engine kernel@grid@kK (bench.launch_key; K =
+            steps per launch: K for k_rollout, 1 otherwise), the longest
+            run's traced duration stats and -- given the JSON line of the
+            traced bench run after a colon -- that run's p_lock for the key,
+            with bench.kernel_source_sha() of the sources
             (profiles/<TAG>_trace.json, read by bench.py's roofline)
 
 bench.py launches the same kernel in several workloads (the headline's
@@ -49,14 +52,23 @@ def to_json(tag, paths):
     import json
     import os
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import bench
+    from pmc_summary import bench_p_lock
+    rollout_k = 100
+    if "--rollout-k" in paths:
+        i = paths.index("--rollout-k")
+        rollout_k = int(paths[i + 1])
+        paths = paths[:i] + paths[i + 2:]
     longest = {}
-    for path in paths:  # earlier files win ties
+    for spec in paths:  # earlier files win ties
+        path, _, bj = spec.partition(":")
+        pl = bench_p_lock(bj)
         for key, v in split_runs(path):
-            k = f"{key[0]}@{key[1]}"
+            k = f"{key[0]}@{key[1]}@k{rollout_k if key[0].startswith('k_rollout') else 1}"
             if key[0].startswith("k_") and len(v) > longest.get(k, {}).get("launches", 0):
-                longest[k] = dict(stats(v), trace=os.path.basename(path))
-    print(json.dumps({"tag": tag, "kernel_source_sha": bench.kernel_source_sha(),
+                longest[k] = dict(stats(v), trace=os.path.basename(path), p_lock=pl.get(k))
+    print(json.dumps({"tag": tag, "kernel_source_sha": bench.kernel_source_sha(), "rollout_k": rollout_k,
                       "kernels": longest}, indent=1))
 
 
