@@ -23,6 +23,7 @@ struct st_ctx {
     int32_t *stats;
     uint32_t *mt;
     uint32_t *act_flag;  // st_set_action_flag (caller-owned), or null
+    int cus;             // compute units of the device
 };
 
 namespace {
@@ -77,6 +78,7 @@ st::KParams params(const st_ctx *c) {
     p.stats = c->stats;
     p.mt = c->mt;
     p.act_flag = c->act_flag;
+    p.cus = c->cus;
     return p;
 }
 
@@ -122,6 +124,7 @@ int st_create(st_ctx **out, const st_config *cfg, int device, int64_t n_envs) {
     c->device = device;
     if (const char *ab = getenv("ST_ABLATE")) c->ablate = (uint32_t)strtoul(ab, nullptr, 0);
     c->n = n_envs;
+    if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) c->cus = 0;
     c->stride = (n_envs + st::kWave - 1) / st::kWave * st::kWave;
     const size_t sd = (size_t)c->stride;
     hipError_t e = hipSuccess;

@@ -17,10 +17,12 @@ constexpr int kMtN = 624;
 constexpr int64_t kMtPitch = 2 * kMtN + 16;
 // after the last env: a draw window reads up to 16 words past index 623 of B
 constexpr int64_t kMtPadBack = 64;
-// diagnostic stamps per workgroup: logic wave 10 s_memtime phase stamps,
-// s_memrealtime at start and end, HW_ID, XCC_ID, draw kind (words 0-15); draw
-// wave 12 stamps + s_memrealtime at start and end (words 16-31)
-constexpr int kStampWords = 32;
+// diagnostic stamps per workgroup: st_step: logic wave 10 s_memtime phase
+// stamps, s_memrealtime at start and end, HW_ID, XCC_ID, draw kind (words
+// 0-15); draw wave 12 stamps + s_memrealtime at start and end (words 16-31);
+// st_rollout: per-phase cycle totals of the logic / draw / output wave
+// (words 0-15 / 16-31 / 32-47)
+constexpr int kStampWords = 48;
 constexpr int kPieceRow = ST_STAT_PIECE;     // rows 0..14 (counters + piece) move every step
 constexpr int kHotRows = ST_STAT_PIECE + 1;
 constexpr int kHotQ = (kHotRows * 16 + kWave - 1) / kWave;  // 16-B slots per lane
@@ -53,6 +55,7 @@ struct KParams {
     int32_t *reward;         // [n]
     uint8_t *done;           // [n]
     uint32_t *act_flag;      // st_set_action_flag: sticky "action outside 0..6" word, or null
+    int32_t cus;             // compute units of the device (launch_rollout's kernel choice)
 };
 
 hipError_t launch_seed(const KParams &p, hipStream_t s);

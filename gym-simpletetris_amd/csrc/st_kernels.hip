@@ -474,10 +474,12 @@ __device__ __attribute__((noinline)) void mt_finish(uint32_t *g, uint32_t *S, in
 // continue in the loop, switching generations at index 624.
 // COUNT: also count the drawn shape in cnt (a spawn's _new_piece :199; not
 // for a preview, which is counted when it spawns).
+// pre_pg: the next generation's progress when `pre` was loaded (-1: now);
+// its words past index 623 are usable only if that generation was complete.
 template <int WIN, bool COUNT = true>
 __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t &mtst,
                                           uint32_t *mt_wave, uint32_t *S, int lane,
-                                          const MtPre &pre, bool have_pre) {
+                                          const MtPre &pre, bool have_pre, int pre_pg = -1) {
     int32_t maxc = cnt[0], sumc = cnt[0];
 #pragma unroll
     for (int i = 1; i < 7; ++i) {
@@ -495,7 +497,7 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
         // The prefetched words sit at positions idx.. of the current
         // generation and, past 623, of the next one (cur[624..639] is
         // next[0..15], see the layout) -- usable there once it is complete.
-        const int lim = pg == kMtN ? kMtN + WIN : kMtN;
+        const int lim = (pre_pg < 0 ? pg : pre_pg) == kMtN ? kMtN + WIN : kMtN;
         int pos = idx;  // words consumed, counted from the current generation's start
         // NW words w[0..NW) at positions p0.. (lanes continuing at p0 only)
         auto pass = [&](const uint32_t *w, int p0, auto nwc) {
@@ -600,11 +602,19 @@ __device__ __forceinline__ uint32_t pack_piece(int id, int rot, int ax, int ay, 
 
 // ---------------------------------------------------------------- step
 // In-kernel phase stamps (diagnostic instantiation only; MI355X guide §7).
+// st_step: the time at each stamp; st_rollout: the cycles from the previous
+// stamp, summed over the launch's steps (per-phase totals, uint32).
 #define ST_STAMP(i)                                                    \
     do {                                                               \
         if constexpr (STAMP) {                                         \
             __builtin_amdgcn_sched_barrier(0);                         \
-            tstamp[i] = __builtin_amdgcn_s_memtime();                  \
+            const uint64_t now_ = __builtin_amdgcn_s_memtime();        \
+            if constexpr (KSTEPS == 1) {                               \
+                tstamp[i] = now_;                                      \
+            } else {                                                   \
+                tacc[i] += (uint32_t)(now_ - tlast);                   \
+                tlast = now_;                                          \
+            }                                                          \
             __builtin_amdgcn_sched_barrier(0);                         \
         }                                                              \
     } while (0)
@@ -700,6 +710,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
     constexpr bool DO_D = ROLE != kRoleL;  // MT words, next-generation block, draws
     constexpr bool TWO = ROLE != kRoleOne;
     [[maybe_unused]] uint64_t tstamp[12] = {};
+    [[maybe_unused]] uint32_t tacc[12] = {};  // rollout stamp build: per-phase cycle totals
+    [[maybe_unused]] uint64_t tlast = 0;
     [[maybe_unused]] uint64_t draw_kind = 0;  // stamp build: 1 = a lane twisted, 2 = a draw ran past 8 words
     constexpr bool S32 = HT != 0 && HT <= 25;  // see pc_bits
     const uint32_t kFlags = SC0 ? (p.flags & (ST_REWARD_STEP | ST_STEP_RESET)) : p.flags;
@@ -713,7 +725,10 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
     constexpr uint32_t kAblate = 0u;
 #endif
     [[maybe_unused]] uint64_t rt0 = 0;
-    if constexpr (STAMP) rt0 = __builtin_amdgcn_s_memrealtime();
+    if constexpr (STAMP) {
+        rt0 = __builtin_amdgcn_s_memrealtime();
+        tlast = __builtin_amdgcn_s_memtime();
+    }
     ST_STAMP(0);
     uint32_t *const L = sm.L;
     uint32_t *const SS = sm.SS;
@@ -851,7 +866,6 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
     }
     auto ss = [&](int r) -> uint32_t & { return SS[r * kWave + lane]; };
     auto tab = [&](int i) -> uint2 { return *reinterpret_cast<const uint2 *>(&sm.T2[2 * i]); };
-
     // an action outside value_action_map in any step of this launch (the
     // reference's KeyError, tetris_env.py:245; the step treats it as idle)
     [[maybe_unused]] bool bad_act = false;
@@ -875,7 +889,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
     // bits; in a two-wave step the draw wave replaces the row after B1, and in
     // a two-wave rollout it hands step t-1's word over in mtw: read after B1)
     uint32_t mt0 = ss(ST_STAT_MT_INDEX);
-    if constexpr (STAMP) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if constexpr (STAMP && KSTEPS == 1) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     ST_STAMP(1);
 
     uint2 desc = make_uint2(0u, 0u);
@@ -942,7 +956,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
             }
         }
         wg_barrier();  // B1: the draw wave learns which lanes lock
-        if constexpr (DO_D) ST_STAMP(10);
+        if constexpr (DO_D || KSTEPS != 1) ST_STAMP(10);
         if constexpr (DO_D && ST_DPRIO > 0) __builtin_amdgcn_s_setprio(ST_DPRIO);
         if constexpr (DO_L && ST_LPRIO > 0) __builtin_amdgcn_s_setprio(ST_LPRIO);
         if constexpr (DO_D) {
@@ -1425,6 +1439,19 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         buf_store16<kNT>(rs, st ? soff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff,
                          *reinterpret_cast<const uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]));
     }
+    if constexpr (STAMP && KSTEPS != 1) {
+        // rollout stamp build: words [0, 16) of the workgroup's slot the
+        // logic wave's per-phase cycle totals (stamp index i), [16, 32) the
+        // draw wave's; word 12 / 28: s_memrealtime span, 13 / 29: steps
+        ST_STAMP(6);
+        uint64_t *slot = p.stamps + (int64_t)blockIdx.x * kStampWords + (ROLE == kRoleD ? 16 : 0);
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < 12; ++i) slot[i] = tacc[i];
+            slot[12] = __builtin_amdgcn_s_memrealtime() - rt0;
+            slot[13] = (uint64_t)K;
+        }
+    }
     if constexpr (STAMP && KSTEPS == 1) {
         // words [0, 16) of the workgroup's slot: the logic wave (stamps
         // 0-9, realtime start/end, HW_ID, XCC_ID, draw kind); [16, 32): the
@@ -1460,9 +1487,710 @@ __global__ __launch_bounds__(2 * kWave) void k_step(KParams p) {
     else run_steps<WT, HT, F32, STAMP, 1, SC0, kRoleD>(p, sm);
 }
 
-// st_rollout: the same two waves, handing off once per step.
+// ---------------------------------------------------------------- rollout
+// st_rollout: K consecutive TetrisEngine.step calls (tetris_env.py:243-304)
+// in one launch, THREE waves per 64 envs:
+//   logic  (L): action + gravity + lock decision, lock path (paint, full rows,
+//               compaction, holes / height, scoring, death), reward / done,
+//               spawn; state in registers (piece word, clock, counters and the
+//               piece's four rotation descriptors), the board in LDS;
+//   draw   (D): the piece draw (one spawn ahead, as in st_step), its MT
+//               window in registers (reloaded for the position it commits at
+//               the end of every step, so a draw never waits for memory), the
+//               shape counts and MT word in registers, the next-generation
+//               chunk;
+//   output (O): the observation of every step -- the board plane OR'ed with
+//               an overlay plane OV the logic wave writes (the current piece's
+//               cells, or for an env reset in this step its whole terminal
+//               board) -- packed and float32 stores, then OV cleared.
+// One s_barrier per step (B1: the lock mask, logic -> draw, and the pace of
+// all three); one-way LDS flags for the rest: fo (logic -> output: step t's
+// board and overlay are final), f1 (logic -> draw, deaths without
+// auto-reset), f2 (draw -> logic, the rare first draw).  The output wave
+// reads step t's planes before B1(t+1) and the logic wave modifies them only
+// after it, so the obs of step t overlaps the logic wave's action phase of
+// step t+1.  (The two-wave rollout measured 4,160 cycles per step with the
+// logic wave's chain critical -- it also painted, stored and erased the obs
+// overlay -- and the draw wave waiting 1,150 cycles for its window:
+// tools/ro_stamps.py)
+constexpr int kRoleO = 3;
+// issue priorities of the rollout's waves (A/B knobs)
+// (the logic wave's chain sets the step: at 3 against 0, -6% per step,
+// tools/ab_libs_ro.sh)
+#ifndef ST_RO_LPRIO
+#define ST_RO_LPRIO 3
+#endif
+#ifndef ST_RO_DPRIO
+#define ST_RO_DPRIO ST_DPRIO
+#endif
+#ifndef ST_RO_OPRIO
+#define ST_RO_OPRIO 0
+#endif
+// the draw wave's MT windows: 1 = every lane's window reloaded at the end of
+// each step (in registers when a lane locks), 0 = loaded after B1 for the
+// locking lanes only
+#ifndef ST_RO_RWIN
+#define ST_RO_RWIN 1
+#endif
+template <int WT, bool F32>
+struct RoLds {
+    static constexpr int kCols = (WT ? WT : kMaxW) + 2 * kPad;
+    uint32_t L[kCols * kWave] __attribute__((aligned(16)));   // board columns, walls at both ends
+    uint32_t OV[kCols * kWave] __attribute__((aligned(16)));  // obs overlay plane (walls never set)
+    uint32_t SS[kHotQ * 4 * kWave] __attribute__((aligned(16)));  // staged counter rows (prologue / epilogue)
+    uint32_t T2[2 * 28] __attribute__((aligned(8)));              // piece table {m, g}
+    uint32_t S[kMtN];                                             // mt_finish scratch
+    uint32_t O[F32 ? kWave * (kMaxW + 1) : 1];                    // float32 writer staging
+    float F4[F32 ? 64 : 4] __attribute__((aligned(16)));
+    uint32_t lockm[2][2], drawm[2];
+    uint32_t pick1[kWave];
+    uint32_t mtw[2][kWave];  // the draw wave's MT word after step t (step-parity double buffer)
+    uint32_t f1, f2, fo;
+};
+
+// d[r] by selects on values (a select between two array elements would be
+// a pointer select, which puts the array in scratch memory)
+__device__ __forceinline__ uint2 sel4(const uint2 (&d)[4], int r) {
+    const bool b0 = r & 1, b1 = r & 2;
+    const uint32_t ax = b0 ? d[1].x : d[0].x, ay = b0 ? d[1].y : d[0].y;
+    const uint32_t bx = b0 ? d[3].x : d[2].x, by = b0 ? d[3].y : d[2].y;
+    return make_uint2(b1 ? bx : ax, b1 ? by : ay);
+}
+
+template <int WT, int HT, bool F32, bool SC0, bool STAMP, int ROLE>
+__device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &sm) {
+    constexpr bool S32 = HT != 0 && HT <= 25;  // see pc_bits
+    const uint32_t kFlags = SC0 ? (p.flags & (ST_REWARD_STEP | ST_STEP_RESET)) : p.flags;
+#if defined(ST_ABLATION) && ST_ABLATION
+    const uint32_t kAblate = p.ablate;
+#else
+    constexpr uint32_t kAblate = 0u;
+#endif
+    // diagnostic build: per-phase cycle totals over the launch (stamp index i
+    // = the phase that ends there), words [16 * role, 16 * role + 12) of the
+    // workgroup's slot, + s_memrealtime span and the step count
+    [[maybe_unused]] uint32_t tacc[12] = {};
+    [[maybe_unused]] uint64_t tlast = 0, rt0 = 0;
+    auto stamp = [&](int i) {
+        if constexpr (STAMP) {
+            __builtin_amdgcn_sched_barrier(0);
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            tacc[i] += (uint32_t)(now - tlast);
+            tlast = now;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    if constexpr (STAMP) {
+        rt0 = __builtin_amdgcn_s_memrealtime();
+        tlast = __builtin_amdgcn_s_memtime();
+    }
+    uint32_t *const L = sm.L;
+    uint32_t *const OV = sm.OV;
+    uint32_t *const SS = sm.SS;
+    const int W = WT ? WT : p.W;
+    const int H = HT ? HT : p.H;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t e0 = (int64_t)blockIdx.x * kWave;
+    const int64_t e = e0 + lane;
+    const int64_t sd = p.stride;
+    const bool real = e < p.n;
+    const uint32_t hmask = (1u << H) - 1u;
+    const uint32_t floorb = ~hmask;
+    const int K = p.k;
+    const int lrow = lane >> 4, lcc = 4 * (lane & 15);  // transposed 16-B slot: row-in-group, env
+    constexpr int NBQ = ((WT ? WT : kMaxW) + 3) / 4;
+    const uint32_t loff = (uint32_t)lrow * (uint32_t)sd + 4u * (uint32_t)(lane & 15);
+    auto clamp_off = [&](int q, int nrows) -> uint32_t {
+        const int r = 4 * q + lrow < nrows ? lrow : nrows - 1 - 4 * q;
+        return (uint32_t)r * (uint32_t)sd + 4u * (uint32_t)(lane & 15);
+    };
+    auto ss = [&](int r) -> uint32_t & { return SS[r * kWave + lane]; };
+    auto tab = [&](int i) -> uint2 { return *reinterpret_cast<const uint2 *>(&sm.T2[2 * i]); };
+    auto col = [&](uint32_t *P, int x) -> uint32_t & { return P[(x + kPad) * kWave + lane]; };
+
+    // ---- prologue: state into LDS (16 B per lane, transposed), B0 ----
+    // logic: board + counter groups 0-1 (time .. count1); draw: counter
+    // groups 2-3 (count2 .. MT word, piece), the walls, the piece table;
+    // output: the zeroed overlay plane
+    const uint32_t *bsrc = p.board + e0;
+    const uint32_t *ssrc = reinterpret_cast<const uint32_t *>(p.stats) + e0;
+    if constexpr (ROLE == kRoleL) {
+        uint4 bv[NBQ], sv[2];
+#pragma unroll
+        for (int q = 0; q < NBQ; ++q)
+            if (WT || 4 * q < W)
+                bv[q] = *reinterpret_cast<const uint4 *>(bsrc + (size_t)(4 * q) * sd +
+                                                         (4 * q + 4 <= W ? loff : clamp_off(q, W)));
+#pragma unroll
+        for (int q = 0; q < 2; ++q) sv[q] = *reinterpret_cast<const uint4 *>(ssrc + (size_t)(4 * q) * sd + loff);
+#pragma unroll
+        for (int q = 0; q < NBQ; ++q) {
+            if (WT || 4 * q < W) {
+                uint4 v = bv[q];
+                v.x |= floorb;
+                v.y |= floorb;
+                v.z |= floorb;
+                v.w |= floorb;
+                // rows >= W (allocation padding) are not staged (the draw
+                // wave writes the wall columns in the same prologue)
+                if (4 * q + lrow < W) *reinterpret_cast<uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]) = v;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) *reinterpret_cast<uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]) = sv[q];
+        if (lane == 0) sm.fo = 0u;
+    } else if constexpr (ROLE == kRoleD) {
+        uint4 sv[2];
+#pragma unroll
+        for (int q = 2; q < kHotQ; ++q)
+            sv[q - 2] = *reinterpret_cast<const uint4 *>(ssrc + (size_t)(4 * q) * sd +
+                                                         (4 * q + 4 <= kHotRows ? loff : clamp_off(q, kHotRows)));
+        uint32_t tab_m = 0, tab_g = 0;
+#pragma unroll
+        for (int i = 0; i < 28; ++i) {
+            asm("v_writelane_b32 %0, %1, %2" : "+v"(tab_m) : "s"(kTab.m[i]), "i"(i));
+            asm("v_writelane_b32 %0, %1, %2" : "+v"(tab_g) : "s"(kTab.g[i]), "i"(i));
+        }
+#pragma unroll
+        for (int x = 0; x < kPad; ++x) {
+            L[x * kWave + lane] = ~0u;
+            L[(W + kPad + x) * kWave + lane] = ~0u;
+        }
+        if (lane < 28) {
+            sm.T2[2 * lane] = tab_m;
+            sm.T2[2 * lane + 1] = tab_g;
+        }
+        if constexpr (F32) {
+            if (lane < 16) {
+                sm.F4[4 * lane] = (float)(lane & 1);
+                sm.F4[4 * lane + 1] = (float)((lane >> 1) & 1);
+                sm.F4[4 * lane + 2] = (float)((lane >> 2) & 1);
+                sm.F4[4 * lane + 3] = (float)((lane >> 3) & 1);
+            }
+        }
+#pragma unroll
+        for (int q = 2; q < kHotQ; ++q) *reinterpret_cast<uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]) = sv[q - 2];
+        if (lane == 0) {
+            sm.f1 = 0u;
+            sm.f2 = 0u;
+        }
+    } else {
+        for (int i = lane; i < RoLds<WT, F32>::kCols * kWave; i += kWave) OV[i] = 0u;
+    }
+    wg_barrier();  // B0
+    stamp(0);
+    if constexpr (ROLE == kRoleL && ST_RO_LPRIO > 0) __builtin_amdgcn_s_setprio(ST_RO_LPRIO);
+    if constexpr (ROLE == kRoleO && ST_RO_OPRIO > 0) __builtin_amdgcn_s_setprio(ST_RO_OPRIO);
+
+    if constexpr (ROLE == kRoleL) {
+        // ================================================================ logic
+        uint32_t pw = ss(kPieceRow);
+        int32_t time = (int32_t)ss(ST_STAT_TIME);
+        int32_t score = (int32_t)ss(ST_STAT_SCORE), lines = (int32_t)ss(ST_STAT_LINES);
+        int32_t holes = (int32_t)ss(ST_STAT_HOLES), height = (int32_t)ss(ST_STAT_PIECE_HEIGHT);
+        int32_t deaths = (int32_t)ss(ST_STAT_DEATHS);
+        uint32_t mt0 = ss(ST_STAT_MT_INDEX);  // the preview bits of the draw wave's word
+        uint2 d4[4];                          // the current piece's four rotations
+#pragma unroll
+        for (int r = 0; r < 4; ++r) d4[r] = tab((int)(pw & 7u) * 4 + r);
+        uint32_t act_next = p.actions[real ? e : p.n - 1];
+        bool bad_act = false;
+        for (int t = 0; t < K; ++t) {
+            const uint32_t act = real ? act_next : 6u;
+            bad_act |= act > 6u;
+            if (t + 1 < K) act_next = p.actions[(int64_t)(t + 1) * p.n + (real ? e : p.n - 1)];
+            int rot = (int)((pw >> 3) & 3u);
+            int ax = (int)((pw >> 5) & 63u);
+            int ay = (int)((pw >> 11) & 63u);
+            int lock = (int)(pw >> 17);
+            stamp(1);
+            // ---- action (tetris_env.py:245; value_action_map :152-160) + drop ----
+            // both descriptors from registers: the columns are one LDS round trip
+            const bool tries = act == 0u || act == 1u || act == 4u || act == 5u;
+            const int cx = ax + (act == 0u ? -1 : (act == 1u ? 1 : 0));
+            const int cr = act == 4u ? ((rot + 1) & 3) : (act == 5u ? ((rot + 3) & 3) : rot);
+            uint2 desc = sel4(d4, rot);
+            const uint2 cdesc = sel4(d4, cr);
+            uint32_t cur[4], cand[4];
+            read_cols(L, lane, desc.y, ax, cur);
+            read_cols(L, lane, cdesc.y, cx, cand);
+            const bool ok = tries && !collides_v<S32>(cdesc.x, ay, cand);
+            ax = ok ? cx : ax;
+            rot = ok ? cr : rot;
+            desc.x = ok ? cdesc.x : desc.x;
+            desc.y = ok ? cdesc.y : desc.y;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) cur[j] = ok ? cand[j] : cur[j];
+            int d = drop_v(desc.y, ay, cur);
+            if (act == 2u) {                  // hard_drop :54-59
+                ay += d;
+                d = 0;
+            } else if (act == 3u && d > 0) {  // soft_drop :49-51
+                ay += 1;
+                d -= 1;
+            }
+            // ---- gravity + lock delay (tetris_env.py:247-262) ----
+            if (d > 0) {
+                ay += 1;
+                d -= 1;
+                if (kFlags & ST_STEP_RESET) lock = 0;
+            }
+            time += 1;
+            int32_t rew = (kFlags & ST_REWARD_STEP) ? 1 : 0;
+            bool locknow = false;
+            if (d == 0) {
+                const int l1 = lock + 1;
+                lock = l1 < p.lock_mod ? l1 : (l1 == p.lock_mod ? 0 : l1 % p.lock_mod);
+                locknow = lock == 0 && !(kAblate & 1u);
+            }
+            stamp(2);
+            {
+                const uint64_t m = __ballot(locknow);
+                if (lane == 0) {
+                    sm.lockm[t & 1][0] = (uint32_t)m;
+                    sm.lockm[t & 1][1] = (uint32_t)(m >> 32);
+                }
+            }
+            wg_barrier();  // B1
+            stamp(3);
+            if (t > 0) mt0 = sm.mtw[(t - 1) & 1][lane];  // the draw wave's word after step t-1
+            // the preview's descriptors, for a spawn below (read under the lock path)
+            uint2 s4[4];
+            const int pvid = pv_ok(mt0) ? pv_id(mt0) : 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s4[r] = tab(pvid * 4 + r);
+
+            // ---- lock path (tetris_env.py:263-299) ----
+            bool died = false, spawn = false;
+            [[maybe_unused]] uint32_t tb[WT ? WT : 1];  // the board after the lock (a reset copies it to OV)
+            if (locknow) {
+                paint<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
+                uint32_t andv = ~0u, orv = 0, sctz = 0, spop = 0;
+                if constexpr (WT != 0) {
+#pragma unroll
+                    for (int x = 0; x < WT; ++x) {
+                        const uint32_t v = col(L, x);
+                        tb[x] = v;
+                        andv &= v;
+                        orv |= v;
+                        sctz += __builtin_ctz(v);
+                        spop += __builtin_popcount(v);
+                    }
+                } else {
+#pragma unroll 8
+                    for (int x = 0; x < W; ++x) {
+                        const uint32_t v = col(L, x);
+                        andv &= v;
+                        orv |= v;
+                        sctz += __builtin_ctz(v);
+                        spop += __builtin_popcount(v);
+                    }
+                }
+                andv &= hmask;
+                int32_t ncl = 0;
+                if (andv) {  // full rows: compact, recount (_clear_lines :205-216)
+                    ncl = __builtin_popcount(andv);
+                    orv = 0;
+                    sctz = spop = 0;
+                    if constexpr (WT != 0) {
+                        uint32_t c[WT];
+#pragma unroll
+                        for (int x = 0; x < WT; ++x) c[x] = col(L, x) & hmask;
+                        uint32_t full = andv;
+                        while (full) {
+                            const int r = __builtin_ctz(full);
+                            full &= full - 1u;
+                            const uint32_t above = (1u << r) - 1u;
+                            const uint32_t keep = ~(above | (1u << r));
+#pragma unroll
+                            for (int x = 0; x < WT; ++x) c[x] = (c[x] & keep) | ((c[x] & above) << 1);
+                        }
+#pragma unroll
+                        for (int x = 0; x < WT; ++x) {
+                            const uint32_t v = c[x] | floorb;
+                            tb[x] = v;
+                            col(L, x) = v;
+                            orv |= v;
+                            sctz += __builtin_ctz(v);
+                            spop += __builtin_popcount(v);
+                        }
+                    } else {
+#pragma unroll 8
+                        for (int x = 0; x < W; ++x) {
+                            const uint32_t v = compact(col(L, x) & hmask, andv) | floorb;
+                            col(L, x) = v;
+                            orv |= v;
+                            sctz += __builtin_ctz(v);
+                            spop += __builtin_popcount(v);
+                        }
+                    }
+                    lines += ncl;
+                }
+                orv &= hmask;
+                const int32_t nh = W * H - (int32_t)sctz - ((int32_t)spop - W * (32 - H));  // _count_holes :218-220
+                if (kFlags & ST_ADVANCED_CLEARS) {  // :266-269
+                    constexpr uint64_t kClr = (40ull << 12) | (100ull << 24) | (300ull << 36) | (1200ull << 48);
+                    const int32_t sc = ncl <= 4 ? (int32_t)((kClr >> (12 * ncl)) & 0xFFFu) : 0;
+                    rew += (sc * 5) / 2;
+                    score += sc;
+                } else if (kFlags & ST_HIGH_SCORING) {  // :270-272
+                    rew += 1000 * ncl;
+                    score += ncl;
+                } else {  // :273-275
+                    rew += 100 * ncl;
+                    score += ncl;
+                }
+                if (orv & 1u) {  // death :277-281
+                    holes = nh;
+                    deaths += 1;
+                    died = true;
+                    rew = -100;
+                } else {  // :283-299
+                    const int32_t old_holes = holes;
+                    holes = nh;
+                    const int32_t hgt = __builtin_popcount(orv);
+                    if (kFlags & ST_PENALISE_HEIGHT) {
+                        rew -= hgt;
+                    } else if (kFlags & ST_PENALISE_HEIGHT_INCREASE) {
+                        if (hgt > height) rew -= 10 * (hgt - height);
+                        height = hgt;
+                    }
+                    if (kFlags & ST_PENALISE_HOLES) rew -= 5 * holes;
+                    else if (kFlags & ST_PENALISE_HOLES_INCREASE) rew -= 5 * (holes - old_holes);
+                    spawn = true;
+                }
+            }
+            stamp(4);
+            const bool reset_now = died && p.autoreset == ST_AUTORESET_SAME_STEP;
+            const bool draw = spawn || reset_now;  // the lock consumed the preview
+            if (p.autoreset != ST_AUTORESET_SAME_STEP) {  // deaths keep the preview: tell the draw wave
+                const uint64_t m = __ballot(draw);
+                if (lane == 0) {
+                    sm.drawm[0] = (uint32_t)m;
+                    sm.drawm[1] = (uint32_t)(m >> 32);
+                    lds_flag_set(&sm.f1, (uint32_t)t + 1u);
+                }
+            }
+            {
+                const auto rr = buf_rsrc(p.reward ? p.reward + (int64_t)t * p.n : nullptr, (uint32_t)p.n * 4u);
+                const auto rd = buf_rsrc(p.done ? p.done + (int64_t)t * p.n : nullptr, (uint32_t)p.n);
+                __builtin_amdgcn_raw_buffer_store_b32(rew, rr, real ? (uint32_t)e * 4u : kOff, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((char)(died ? 1 : 0), rd, real ? (uint32_t)e : kOff, 0, 0);
+            }
+            // spawn id: the preview; a lane without one takes the draw wave's first draw (rare)
+            int sid = pvid;
+            {
+                const bool need1 = draw && !pv_ok(mt0);
+                if (__ballot(need1)) {
+                    lds_flag_wait(&sm.f2, (uint32_t)t + 1u);
+                    if (need1) sid = (int)sm.pick1[lane];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const uint2 v = tab(sid * 4 + r);
+                        s4[r].x = need1 ? v.x : s4[r].x;
+                        s4[r].y = need1 ? v.y : s4[r].y;
+                    }
+                }
+            }
+            stamp(5);
+            // ---- this step's obs (tetris_env.py:301-302) for the output wave ----
+            // a death without auto-reset: the board loses the piece (R8,
+            // _set_piece(False), :303), the obs keeps it (overlay); a death
+            // with auto-reset: the obs is the whole terminal board (overlay
+            // plane), the board becomes empty (clear(), :306-315)
+            if (died && !reset_now) erase<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
+            const uint2 od = make_uint2(spawn ? s4[0].x : desc.x, spawn ? s4[0].y : desc.y);
+            const int oax = spawn ? W / 2 : ax, oay = spawn ? 0 : ay;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                OV[(oax + pc_dx(od.y, j) + kPad) * kWave + lane] = pc_bits<S32>(od.x, j, oay) & hmask;
+            if (reset_now) {
+                if constexpr (WT != 0) {
+#pragma unroll
+                    for (int x = 0; x < WT; ++x) {
+                        col(OV, x) = tb[x] & hmask;
+                        col(L, x) = floorb;
+                    }
+                } else {
+                    for (int x = 0; x < W; ++x) {
+                        col(OV, x) = col(L, x) & hmask;
+                        col(L, x) = floorb;
+                    }
+                }
+            }
+            {
+                // the finished episode's counters (ST_AUTORESET_SAME_STEP):
+                // unconditional buffer stores, dropped (out-of-range offset)
+                // for lanes that did not reset -- a store under a branch would
+                // leave the compiler's vmcnt count unknown at the next step's
+                // action-load wait, which then waited for this step's stores
+                const auto rs = buf_rsrc(p.stats, (uint32_t)ST_NSTAT * (uint32_t)sd * 4u);
+                const uint32_t eo = (uint32_t)e * 4u;
+                auto put = [&](int row, int32_t v) {
+                    __builtin_amdgcn_raw_buffer_store_b32(v, rs, reset_now ? eo + (uint32_t)row * (uint32_t)sd * 4u : kOff,
+                                                          0, 0);
+                };
+                put(ST_STAT_EP_TIME, time);
+                put(ST_STAT_EP_SCORE, score);
+                put(ST_STAT_EP_LINES, lines);
+                put(ST_STAT_EP_HOLES, holes);
+                if (reset_now) time = score = lines = holes = height = 0;
+            }
+            if (lane == 0) lds_flag_set(&sm.fo, (uint32_t)t + 1u);
+            // ---- state for the next step ----
+            pw = pack_piece(draw ? sid : (int)(pw & 7u), draw ? 0 : rot, draw ? W / 2 : ax, draw ? 0 : ay, lock);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                d4[r].x = draw ? s4[r].x : d4[r].x;
+                d4[r].y = draw ? s4[r].y : d4[r].y;
+            }
+            stamp(6);
+        }
+        wg_barrier();  // the output wave has read the last step's planes
+        // ---- epilogue: board and the rows this wave owns ----
+        __builtin_amdgcn_raw_buffer_store_b32(1u, buf_rsrc(p.act_flag, 4u), bad_act ? 0u : kOff, 0, 0);
+        ss(ST_STAT_TIME) = (uint32_t)time;
+        ss(ST_STAT_SCORE) = (uint32_t)score;
+        ss(ST_STAT_LINES) = (uint32_t)lines;
+        ss(ST_STAT_HOLES) = (uint32_t)holes;
+        ss(ST_STAT_PIECE_HEIGHT) = (uint32_t)height;
+        ss(ST_STAT_DEATHS) = (uint32_t)deaths;
+        ss(kPieceRow) = pw;
+        wave_sync();
+        const auto rb = buf_rsrc(p.board, (uint32_t)((W + 3) & ~3) * (uint32_t)sd * 4u);
+        const uint32_t boff = (uint32_t)e0 * 4u + loff * 4u;
+#pragma unroll
+        for (int q = 0; q < NBQ; ++q) {
+            if ((WT || 4 * q < W) && 4 * q + lrow < W) {
+                uint4 v = *reinterpret_cast<const uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]);
+                v.x &= hmask;
+                v.y &= hmask;
+                v.z &= hmask;
+                v.w &= hmask;
+                buf_store16<kNT>(rb, boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u, v);
+            }
+        }
+    } else if constexpr (ROLE == kRoleD) {
+        // ================================================================ draw
+        const MtRes mrs = mt_res(p.mt + e0 * kMtPitch, lane);
+        uint32_t mtw_r = ss(ST_STAT_MT_INDEX);
+        int32_t cnt_r[7];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) cnt_r[i] = (int32_t)ss(ST_STAT_COUNT0 + i);
+        MtPre win;
+        int win_pg = -1;
+        if constexpr (ST_RO_RWIN) {
+            mt_pre_load<kMtWin>(mrs, mtw_r, real, win);
+            win_pg = (int)((mtw_r >> 10) & 0x3FFu);
+        }
+        for (int t = 0; t < K; ++t) {
+            const uint32_t mt0 = mtw_r;
+            stamp(1);
+            // this step's next-generation chunk: operands issued before B1
+            MtChunk chunk;
+            mt_chunk_issue(mrs, mt0, real && !(kAblate & 2u), lane, chunk);
+            stamp(2);
+            wg_barrier();  // B1
+            stamp(3);
+            if constexpr (ST_RO_DPRIO > 0) __builtin_amdgcn_s_setprio(ST_RO_DPRIO);
+            bool locknow;
+            {
+                const uint32_t w = lane < 32 ? sm.lockm[t & 1][0] : sm.lockm[t & 1][1];
+                locknow = (w >> (lane & 31)) & 1u;
+            }
+            // every locking lane draws (speculatively: a death without
+            // auto-reset keeps its preview, committed below only where the
+            // lock consumed it): the first draw where there is no preview
+            // (rare), then the next preview
+            uint32_t mtst = mt0;
+            int sid = pv_id(mt0);
+            int32_t cnt[7];
+#pragma unroll
+            for (int i = 0; i < 7; ++i) cnt[i] = cnt_r[i];
+            if constexpr (STAMP) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                stamp(4);
+            }
+            uint32_t mt_new = mtst;
+            if constexpr (!ST_RO_RWIN) mt_pre_load<kMtWin>(mrs, mt0, locknow, win);  // locking lanes, after B1
+            if (!(kAblate & 2u)) {
+                mt_win_consume<kMtWin>(win);
+                const bool need1 = locknow && !pv_ok(mt0);
+                if (__ballot(need1)) {  // after st_seed / st_mt_sync / a host-written state
+                    const int pk = draw_shape<kMtWin, false>(need1, cnt, mtst, p.mt + e0 * kMtPitch, sm.S, lane,
+                                                             win, false);
+                    if (need1) sid = pk;
+                }
+                sm.pick1[lane] = (uint32_t)sid;
+                if (lane == 0) lds_flag_set(&sm.f2, (uint32_t)t + 1u);
+#pragma unroll
+                for (int i = 0; i < 7; ++i) cnt[i] += (locknow && i == sid);  // _new_piece :199
+                const uint32_t m0 = mtst;
+                const int npv = draw_shape<kMtWin, false>(locknow, cnt, mtst, p.mt + e0 * kMtPitch, sm.S, lane, win,
+                                                          locknow && pv_ok(mt0), win_pg);
+                mt_new = pv_pack(mtst, npv, mt_consumed(m0, mtst));
+            } else {
+                sm.pick1[lane] = (uint32_t)sid;
+                if (lane == 0) lds_flag_set(&sm.f2, (uint32_t)t + 1u);
+            }
+            const int chunk_pg = mt_chunk_store<0>(mrs, lane, chunk);
+            const bool chunk_me = lane == chunk.l;
+            stamp(5);
+            bool dr = locknow;
+            if (p.autoreset != ST_AUTORESET_SAME_STEP) {
+                lds_flag_wait(&sm.f1, (uint32_t)t + 1u);
+                const uint32_t w = lane < 32 ? sm.drawm[0] : sm.drawm[1];
+                dr = (w >> (lane & 31)) & 1u;
+            }
+            uint32_t mt_out = dr ? mt_new : mt0;
+            if (chunk_me && (mt_out & (1u << 20)) == (mt0 & (1u << 20))) {
+                int i2, pg2, c2;
+                mt_unpack(mt_out, i2, pg2, c2);
+                mt_out = mt_keep(mt_out, mt_pack(i2, chunk_pg, c2));
+            }
+            sm.mtw[t & 1][lane] = mt_out;  // the logic wave reads it after B1(t + 1)
+#pragma unroll
+            for (int i = 0; i < 7; ++i) cnt_r[i] += (dr && i == sid);  // shape_counts[name] += 1, :199
+            mtw_r = mt_out;
+            // next step's windows: the last memory operations of this step
+            // (the progress of before this step's chunk: conservative)
+            if constexpr (ST_RO_RWIN) {
+                mt_pre_load<kMtWin>(mrs, mt_out, real, win);
+                win_pg = (int)((mt0 >> 10) & 0x3FFu);
+            }
+            stamp(6);
+        }
+        wg_barrier();
+#pragma unroll
+        for (int i = 0; i < 7; ++i) ss(ST_STAT_COUNT0 + i) = (uint32_t)cnt_r[i];
+        ss(ST_STAT_MT_INDEX) = mtw_r;
+        wave_sync();
+    } else {
+        // ================================================================ output
+        const bool wide_obs = (p.n & 3) == 0 && e0 + kWave <= p.n && (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0;
+        for (int t = 0; t < K; ++t) {
+            stamp(1);
+            wg_barrier();  // B1 (keeps the pace; the planes of step t-1 were read before it)
+            stamp(2);
+            lds_flag_wait(&sm.fo, (uint32_t)t + 1u);
+            stamp(3);
+            uint32_t *const obs_t = p.obs ? p.obs + (int64_t)t * W * p.n : nullptr;
+            if (obs_t && !(kAblate & 8u)) {
+                if (wide_obs) {
+                    const auto ro = buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u);
+                    const uint32_t noff = (uint32_t)lrow * (uint32_t)p.n + (uint32_t)lcc;
+#pragma unroll
+                    for (int q = 0; q < NBQ; ++q) {
+                        if ((WT || 4 * q < W) && 4 * q + lrow < W) {
+                            const int i = (4 * q + lrow + kPad) * kWave + lcc;
+                            uint4 v = *reinterpret_cast<const uint4 *>(&L[i]);
+                            const uint4 o = *reinterpret_cast<const uint4 *>(&OV[i]);
+                            v.x = (v.x | o.x) & hmask;
+                            v.y = (v.y | o.y) & hmask;
+                            v.z = (v.z | o.z) & hmask;
+                            v.w = (v.w | o.w) & hmask;
+                            buf_store16<kNT>(ro, ((uint32_t)e0 + (uint32_t)(4 * q) * (uint32_t)p.n + noff) * 4u, v);
+                        }
+                    }
+                } else if (real) {  // ragged / unaligned: one dword per row
+                    const auto ro = buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u);
+#pragma unroll 1
+                    for (int x = 0; x < W; ++x)
+                        __builtin_amdgcn_raw_buffer_store_b32((col(L, x) | col(OV, x)) & hmask, ro,
+                                                              ((uint32_t)x * (uint32_t)p.n + (uint32_t)e) * 4u, 0, kNT);
+                }
+            }
+            if constexpr (F32) {
+                // float32 obs [n][W][H] of the wave's envs: one contiguous block,
+                // lane-consecutive float4 chunks, non-temporal (A/B: -13% f32 rollout)
+                const int64_t nreal64 = p.n - e0 < kWave ? p.n - e0 : kWave;
+                const int nreal = (int)nreal64;
+                float *out = p.obs_f32 + ((int64_t)t * p.n + e0) * (W * H);
+                if constexpr (WT != 0 && HT % 4 == 0) {
+                    constexpr int CPC = HT / 4, CPE = WT * CPC;
+                    uint32_t *O = sm.O;
+#pragma unroll
+                    for (int x = 0; x < WT; ++x) O[lane * (WT + 1) + x] = (col(L, x) | col(OV, x)) & hmask;
+                    wave_sync();
+                    float4 *out4 = reinterpret_cast<float4 *>(out);
+                    const float4 *F4 = reinterpret_cast<const float4 *>(sm.F4);
+                    const int total = nreal * CPE;
+                    for (int c = lane; c < total; c += kWave) {
+                        const int ee = c / CPE;
+                        const int cr = c - ee * CPE;
+                        const int x = cr / CPC;
+                        const int q = cr - x * CPC;
+                        const float4 f = F4[(O[ee * (WT + 1) + x] >> (4 * q)) & 15u];
+                        typedef float f32x4 __attribute__((ext_vector_type(4)));
+                        const f32x4 fv = {f.x, f.y, f.z, f.w};
+                        __builtin_nontemporal_store(fv, reinterpret_cast<f32x4 *>(&out4[c]));
+                    }
+                    wave_sync();  // staging reads done before the next step's writes
+                } else {
+                    const int per_env = W * H;
+                    const int total = nreal * per_env;
+                    for (int f = lane; f < total; f += kWave) {
+                        const int ee = f / per_env;
+                        const int rem = f - ee * per_env;
+                        const int x = rem / H;
+                        const int y = rem - x * H;
+                        const uint32_t w = (L[(x + kPad) * kWave + ee] | OV[(x + kPad) * kWave + ee]) & hmask;
+                        out[f] = (float)((w >> y) & 1u);
+                    }
+                }
+            }
+            wave_sync();  // every read of the overlay plane precedes its clearing
+#pragma unroll
+            for (int q = 0; q < NBQ; ++q)
+                if ((WT || 4 * q < W) && 4 * q + lrow < W)
+                    *reinterpret_cast<uint4 *>(&OV[(4 * q + lrow + kPad) * kWave + lcc]) = make_uint4(0u, 0u, 0u, 0u);
+            stamp(4);
+        }
+        wg_barrier();
+    }
+    // ---- counter rows this wave owns (logic: 0-5 and the piece row, draw:
+    // the shape counts and the MT word) ----
+    if constexpr (ROLE != kRoleO) {
+        constexpr uint32_t kRowsD = ((1u << 7) - 1u) << ST_STAT_COUNT0 | 1u << ST_STAT_MT_INDEX;
+        constexpr uint32_t kOwn = ROLE == kRoleD ? kRowsD : ((1u << kHotRows) - 1u) & ~kRowsD;
+        const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
+        const uint32_t soff = (uint32_t)e0 * 4u + loff * 4u;
+#pragma unroll
+        for (int q = 0; q < kHotQ; ++q) {
+            if (((kOwn >> (4 * q)) & 0xFu) == 0u) continue;
+            const bool st = (kOwn >> (4 * q + lrow)) & 1u;
+            buf_store16<kNT>(rs, st ? soff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff,
+                             *reinterpret_cast<const uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]));
+        }
+    }
+    if constexpr (STAMP) {
+        uint64_t *slot = p.stamps + (int64_t)blockIdx.x * kStampWords + 16 * (ROLE == kRoleL ? 0 : ROLE == kRoleD ? 1 : 2);
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < 12; ++i) slot[i] = tacc[i];
+            slot[12] = __builtin_amdgcn_s_memrealtime() - rt0;
+            slot[13] = (uint64_t)K;
+        }
+    }
+}
+
+// (Capping it at 85 VGPRs -- six waves per SIMD, so 131,072 envs fit at once
+// -- spills and loses at 65,536 envs: 1.72 -> 2.08 us per step; launch_rollout
+// runs the two-wave rollout above 4 workgroups per CU instead.)
+template <int WT, int HT, bool F32, bool SC0 = false, bool STAMP = false>
+__global__ __launch_bounds__(3 * kWave) void k_rollout(KParams p) {
+    __shared__ RoLds<WT, F32> sm;
+    if (threadIdx.x < kWave) rollout_wave<WT, HT, F32, SC0, STAMP, kRoleL>(p, sm);
+    else if (threadIdx.x < 2 * kWave) rollout_wave<WT, HT, F32, SC0, STAMP, kRoleD>(p, sm);
+    else rollout_wave<WT, HT, F32, SC0, STAMP, kRoleO>(p, sm);
+}
+
+// The two-wave rollout (run_steps, board and counters in LDS): launch_rollout
+// takes it for batches of more than 4 workgroups per CU, where the three-wave
+// kernel's extra waves and window reloads cost more than its shorter logic
+// chain gains (131,072 envs: 2.8 against 4.0 us per step).
 template <int WT, int HT, bool F32, bool SC0 = false>
-__global__ __launch_bounds__(2 * kWave) void k_rollout(KParams p) {
+__global__ __launch_bounds__(2 * kWave) void k_rollout2(KParams p) {
     __shared__ StepLds<F32, 0> sm;
     if (threadIdx.x < kWave) run_steps<WT, HT, F32, false, 0, SC0, kRoleL>(p, sm);
     else run_steps<WT, HT, F32, false, 0, SC0, kRoleD>(p, sm);
@@ -2174,10 +2902,28 @@ hipError_t launch_render(const KParams &p, hipStream_t s) {
 }
 
 hipError_t launch_rollout(const KParams &p, hipStream_t s) {
-    const dim3 grid((unsigned)(p.stride / kWave)), block(2 * kWave);  // logic + draw wave
     const bool f32 = p.obs_f32 != nullptr;
     const bool sc0 = !(p.flags & kScoringFlags);
-    if (p.W == 10 && p.H == 20) {
+    const int64_t wgs = p.stride / kWave;
+    const dim3 grid((unsigned)wgs);
+    if (wgs > 4 * (int64_t)(p.cus > 0 ? p.cus : 256) && !p.stamps) {
+        const dim3 block(2 * kWave);  // logic + draw wave
+        if (p.W == 10 && p.H == 20) {
+            if (f32 && sc0) hipLaunchKernelGGL((k_rollout2<10, 20, true, true>), grid, block, 0, s, p);
+            else if (f32) hipLaunchKernelGGL((k_rollout2<10, 20, true>), grid, block, 0, s, p);
+            else if (sc0) hipLaunchKernelGGL((k_rollout2<10, 20, false, true>), grid, block, 0, s, p);
+            else hipLaunchKernelGGL((k_rollout2<10, 20, false>), grid, block, 0, s, p);
+        } else {
+            if (f32) hipLaunchKernelGGL((k_rollout2<0, 0, true>), grid, block, 0, s, p);
+            else hipLaunchKernelGGL((k_rollout2<0, 0, false>), grid, block, 0, s, p);
+        }
+        return hipGetLastError();
+    }
+    const dim3 block(3 * kWave);  // logic + draw + output wave
+    if (p.stamps && p.W == 10 && p.H == 20 && !f32) {  // diagnostic phase stamps (ST_STAMPS)
+        if (sc0) hipLaunchKernelGGL((k_rollout<10, 20, false, true, true>), grid, block, 0, s, p);
+        else hipLaunchKernelGGL((k_rollout<10, 20, false, false, true>), grid, block, 0, s, p);
+    } else if (p.W == 10 && p.H == 20) {
         if (f32 && sc0) hipLaunchKernelGGL((k_rollout<10, 20, true, true>), grid, block, 0, s, p);
         else if (f32) hipLaunchKernelGGL((k_rollout<10, 20, true>), grid, block, 0, s, p);
         else if (sc0) hipLaunchKernelGGL((k_rollout<10, 20, false, true>), grid, block, 0, s, p);

@@ -252,6 +252,38 @@ def test_bench_workload_st_rollout(config):
         eng.close()
 
 
+@pytest.mark.parametrize("config", sorted(CONFIGS))
+def test_rollout_large_batch_two_wave_kernel(config):
+    """st_rollout above 4 workgroups per CU runs the two-wave rollout kernel
+    (launch_rollout's choice; the three-wave kernel below it): 2x the CUs'
+    4-workgroup batch plus a ragged tail, 3 launches x 100 steps, every step's
+    outputs and the final state bit-exact against the oracle."""
+    import gym_simpletetris_amd as G
+    dev = torch.device("cuda", 0)
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    n = 2 * 4 * 64 * cus + 37
+    assert n > 4 * 64 * cus
+    kw = CONFIGS[config]
+    eng = G.TetrisBatch(n, autoreset="same_step", seeds=[SEED_BASE + e for e in range(n)],
+                        device=dev, width=W, height=H, **kw)
+    CH, NL = 100, 3
+    acts = torch.empty((CH * NL, n), dtype=torch.uint8, device=dev)
+    for t in range(CH * NL):
+        eng.gen_actions(t, ASEED, out=acts[t])
+    eng.reset()
+    orc = ParallelOracle(n, kw)
+    buf = {}
+    try:
+        for c in range(NL):
+            o, r, d = eng.rollout(acts[c * CH:(c + 1) * CH], obs="packed", out=buf)
+            ref = orc.rollout(c * CH, CH)
+            _compare(c * CH, r.cpu().numpy(), d.cpu().numpy(), o.cpu().numpy().view(np.uint32), ref)
+        _check_final(eng, orc)
+    finally:
+        orc.close()
+        eng.close()
+
+
 @pytest.mark.parametrize("n,steps", [(65537, 600), (1 << 20, 24)])
 def test_ragged_and_large_batches(n, steps):
     """A ragged batch (65,537 envs: the last wave holds one real env, the

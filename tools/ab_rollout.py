@@ -19,7 +19,7 @@ from gym_simpletetris_amd import _lib as C  # noqa: E402
 CH = int(sys.argv[1]) if len(sys.argv) > 1 else 100
 NL = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 F32 = len(sys.argv) > 3 and sys.argv[3] == "f32"
-n = 65536
+n = int(os.environ.get("AB_N", "65536"))
 dev = torch.device("cuda", 0)
 s = torch.cuda.Stream(dev)
 sp = ctypes.c_void_p(s.cuda_stream)

@@ -17,7 +17,7 @@ n = 65536
 b = G.TetrisBatch(n, autoreset="same_step", seeds=[1000 + e for e in range(n)])
 b.reset()
 nw = b.stride // 64
-W = 32  # kStampWords: logic wave words 0-15, draw wave 16-31
+W = 48  # kStampWords: logic wave words 0-15, draw wave 16-31 (32-47: the rollout output wave)
 buf = np.zeros(nw * W, np.uint64)
 rts = []
 # logic wave: stamps 0 1 2 3 8 4 5 6 7 (8 sits between 3 and 4)
