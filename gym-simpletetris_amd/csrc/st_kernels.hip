@@ -135,6 +135,13 @@ constexpr int kNT = 2;
 #ifndef ST_LPRIO
 #define ST_LPRIO 0
 #endif
+// st_step: the obs overlay goes to a plane of its own (OV), so the board and
+// obs rows are read in ONE transposed pass and stored together (A/B, 2 rounds
+// on one box, K = 2,000: 4.82-4.84 -> 4.80-4.81 us; tools/ab_step_libs.sh,
+// profiles/r03/ab_step_k1.txt)
+#ifndef ST_OVPLANE
+#define ST_OVPLANE 1
+#endif
 template <int AUX = 0>
 __device__ __forceinline__ void buf_store16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
     const i32x4 d = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
@@ -623,10 +630,11 @@ __device__ __forceinline__ uint32_t pack_piece(int id, int rot, int ax, int ay, 
 // (the two-wave st_step hands data between them through it).  Plain words
 // only (no vector-type members: a __shared__ object must be trivially
 // constructible).
-template <bool F32, int KSTEPS>
+template <int WT, bool F32, int KSTEPS>
 struct StepLds {
+    static constexpr int kCols = (WT ? WT : kMaxW) + 2 * kPad;
     // board columns L[x + kPad][lane], all-ones walls at both ends
-    uint32_t L[(kMaxW + 2 * kPad) * kWave] __attribute__((aligned(16)));
+    uint32_t L[kCols * kWave] __attribute__((aligned(16)));
     // staged counter rows SS[r][lane] (r < 14: stats rows, 14: piece word)
     uint32_t SS[kHotQ * 4 * kWave] __attribute__((aligned(16)));
     uint32_t T2[2 * 28] __attribute__((aligned(8)));  // piece table {m, g}
@@ -641,6 +649,8 @@ struct StepLds {
     // free transposed reads) and the 16 float4 patterns of a 4-bit nibble
     uint32_t O[F32 ? kWave * (kMaxW + 1) : 1];
     float F4[F32 ? 64 : 4] __attribute__((aligned(16)));
+    // st_step (ST_OVPLANE): the obs overlay plane, laid out like L
+    uint32_t OV[KSTEPS == 1 && ST_OVPLANE ? kCols * kWave : 4] __attribute__((aligned(16)));
     // two-wave st_step hand-offs (see run_steps)
     uint32_t dump[kWave] __attribute__((aligned(16)));  // the logic wave's padding-row writes
     // (step-parity double buffers where a wave may write step t+1's value
@@ -705,7 +715,7 @@ __device__ __forceinline__ void lds_flag_wait(uint32_t *f, uint32_t v) {
 // the rollout loop otherwise holds each flag as a 64-bit lane mask at the
 // SGPR limit, -5% packed rollout; st_step -1%).
 template <int WT, int HT, bool F32, bool STAMP, int KSTEPS, bool SC0, int ROLE>
-__device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS> &sm) {
+__device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KSTEPS> &sm) {
     constexpr bool DO_L = ROLE != kRoleD;  // action, lock path, outputs
     constexpr bool DO_D = ROLE != kRoleL;  // MT words, next-generation block, draws
     constexpr bool TWO = ROLE != kRoleOne;
@@ -754,6 +764,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
     constexpr int NBQ = ((WT ? WT : kMaxW) + 3) / 4;  // board 4-row groups
     const uint32_t *bsrc = p.board + e0;
     const uint32_t *ssrc = reinterpret_cast<const uint32_t *>(p.stats) + e0;
+    constexpr bool OVP = KSTEPS == 1 && ROLE != kRoleOne && ST_OVPLANE;
     auto mine_q = [&](int q) { return ROLE == kRoleOne || (ROLE == kRoleL) == (q < 2); };
     // Rows past the last real row (board padding, counter row 15) re-read the
     // last row -- the same cache line another lane fetches -- instead of
@@ -857,6 +868,12 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
 #pragma unroll
     for (int q = 0; q < kHotQ; ++q)
         if (mine_q(q)) *reinterpret_cast<uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]) = sv[q];
+    if constexpr (OVP && DO_L) {
+#pragma unroll
+        for (int q = 0; q < NBQ; ++q)
+            if ((WT || 4 * q < W) && 4 * q + lrow < W)
+                *reinterpret_cast<uint4 *>(&sm.OV[(4 * q + lrow + kPad) * kWave + lcc]) = make_uint4(0u, 0u, 0u, 0u);
+    }
     if constexpr (TWO) {
         if (ROLE == kRoleL && lane == 0) sm.f1 = 0u;
         if (ROLE == kRoleD && lane == 0) sm.f2 = 0u;
@@ -1124,23 +1141,57 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         // written (buffer stores, see buf_rsrc).
         if (died && !reset_now) erase<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
         if (died) bdirty = ~0u;
+        if constexpr (OVP) {
+            // the overlay of every lane into its own plane: the current piece,
+            // or for a spawn its new piece at the spawn position -- the
+            // preview, known since the step started, or (rare: no preview)
+            // the draw wave's first draw, waited for here
+            int ps = pv_id(mt0);
+            const bool need1 = draw && !pv_ok(mt0);
+            if (__ballot(need1)) {
+                lds_flag_wait(&sm.f2, (uint32_t)t + 1u);
+                if (need1) ps = (int)sm.pick1[lane];
+            }
+            const uint2 pd = tab(ps * 4);
+            const uint32_t om = spawn ? pd.x : desc.x, og = spawn ? pd.y : desc.y;
+            const int ox = spawn ? W / 2 : ax, oy = spawn ? 0 : ay;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                sm.OV[(ox + pc_dx(og, j) + kPad) * kWave + lane] = pc_bits<S32>(om, j, oy) & hmask;
+        }
         sm.KM[lane] = reset_now ? 0u : hmask;
         sm.BD[lane] = bdirty;
         wave_sync();
         const uint4 km = *reinterpret_cast<const uint4 *>(&sm.KM[lcc]);
         const uint4 bd4 = *reinterpret_cast<const uint4 *>(&sm.BD[lcc]);
         const uint32_t bdl = (bd4.x | bd4.y | bd4.z | bd4.w) >> lrow;
-        uint4 bw[NBQ];
+        uint4 bw[NBQ], ow[NBQ];
 #pragma unroll
-        for (int q = 0; q < NBQ; ++q)
-            if (WT || 4 * q < W) bw[q] = *reinterpret_cast<const uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]);
+        for (int q = 0; q < NBQ; ++q) {
+            if (WT || 4 * q < W) {
+                bw[q] = *reinterpret_cast<const uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]);
+                if constexpr (OVP) ow[q] = *reinterpret_cast<const uint4 *>(&sm.OV[(4 * q + lrow + kPad) * kWave + lcc]);
+            }
+        }
         // the board array as one resource: byte offsets < W * stride * 4 <= 2^31
         const auto rb = buf_rsrc(p.board, (uint32_t)W * (uint32_t)sd * 4u);
         const uint32_t boff = ((uint32_t)e0 * 4u + loff * 4u);
+        const bool wide_obs1 = OVP && (p.n & 3) == 0 && e0 + kWave <= p.n &&
+                               (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0;
 #pragma unroll
         for (int q = 0; q < NBQ; ++q) {
             if (WT || 4 * q < W) {
                 uint4 v = bw[q];
+                if constexpr (OVP) {  // obs row: board | overlay (a reset env's terminal board included)
+                    if (p.obs && wide_obs1 && 4 * q + lrow < W) {
+                        const uint4 o = ow[q];
+                        const uint4 ob = make_uint4((v.x | o.x) & hmask, (v.y | o.y) & hmask, (v.z | o.z) & hmask,
+                                                    (v.w | o.w) & hmask);
+                        buf_store16<kNT>(buf_rsrc(p.obs, (uint32_t)W * (uint32_t)p.n * 4u),
+                                         ((uint32_t)e0 + (uint32_t)(4 * q + lrow) * (uint32_t)p.n + (uint32_t)lcc) * 4u,
+                                         ob);
+                    }
+                }
                 v.x &= km.x;
                 v.y &= km.y;
                 v.z &= km.z;
@@ -1150,6 +1201,10 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
                 buf_store16<kNT>(rb, dirty ? boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff, v);
             }
         }
+        if constexpr (OVP) {
+            // (below: the ragged / unaligned obs path and the float32 writer
+            // read the planes per env; nothing is painted into L)
+        } else {
         wave_sync();  // the board reads above precede the overlay paint
         if constexpr (TWO) {
             // the obs overlay of every lane at once: the current piece, or for
@@ -1163,6 +1218,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         } else {
             if (!spawn) paint<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
         }
+        }  // !OVP
     }
 
     ST_STAMP(8);  // (stamp 8: between the early stores and the draw)
@@ -1256,7 +1312,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
             if (__ballot(need1)) {
                 lds_flag_wait(&sm.f2, (uint32_t)t + 1u);
                 if (need1) sid = (int)sm.pick1[lane];
-                if constexpr (KSTEPS == 1) {  // its overlay (the others were painted with the board stores)
+                if constexpr (KSTEPS == 1 && !OVP) {  // its overlay (the others were painted with the board stores)
                     const uint2 sd1 = tab(sid * 4);
                     paint<S32>(L, lane, sd1.x, sd1.y, W / 2, 0, need1 && spawn ? hmask : 0u);
                 }
@@ -1308,7 +1364,9 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
         const bool wide_obs = (p.n & 3) == 0 && e0 + kWave <= p.n &&
                               (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0;
         if (obs_t && !(kAblate & 8u)) {
-            if (wide_obs) {
+            if (OVP && wide_obs) {
+                // stored with the board rows
+            } else if (wide_obs) {
                 const uint32_t noff = (uint32_t)lrow * (uint32_t)p.n + (uint32_t)lcc;
 #pragma unroll
                 for (int q = 0; q < NBQ; ++q) {  // interleaved read/store (measured: reads-first
@@ -1327,8 +1385,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
                 const auto ro = buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u);
 #pragma unroll 1
                 for (int x = 0; x < W; ++x)
-                    __builtin_amdgcn_raw_buffer_store_b32(lcol(L, x, lane) & hmask, ro,
-                                                          ((uint32_t)x * (uint32_t)p.n + (uint32_t)e) * 4u, 0, kNT);
+                    __builtin_amdgcn_raw_buffer_store_b32((lcol(L, x, lane) | (OVP ? lcol(sm.OV, x, lane) : 0u)) & hmask,
+                                                          ro, ((uint32_t)x * (uint32_t)p.n + (uint32_t)e) * 4u, 0, kNT);
             }
         }
         if (F32) {
@@ -1343,7 +1401,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
                 constexpr int CPC = HT / 4, CPE = WT * CPC;
                 uint32_t *O = sm.O;
 #pragma unroll
-                for (int x = 0; x < WT; ++x) O[lane * (WT + 1) + x] = lcol(L, x, lane) & hmask;
+                for (int x = 0; x < WT; ++x)
+                    O[lane * (WT + 1) + x] = (lcol(L, x, lane) | (OVP ? lcol(sm.OV, x, lane) : 0u)) & hmask;
                 wave_sync();
                 float4 *out4 = reinterpret_cast<float4 *>(out);
                 const float4 *F4 = reinterpret_cast<const float4 *>(sm.F4);
@@ -1369,7 +1428,9 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
             } else {
                 const int per_env = W * H;
                 const int total = nreal * per_env;
-                auto word = [&](int ee, int x) { return L[(x + kPad) * kWave + ee] & hmask; };
+                auto word = [&](int ee, int x) {
+                    return (L[(x + kPad) * kWave + ee] | (OVP ? sm.OV[(x + kPad) * kWave + ee] : 0u)) & hmask;
+                };
                 for (int f = lane; f < total; f += kWave) {
                     const int ee = f / per_env;
                     const int rem = f - ee * per_env;
@@ -1482,7 +1543,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<F32, KSTEPS>
 // st_step: two waves per 64 envs (kRoleL, kRoleD), see run_steps.
 template <int WT, int HT, bool F32, bool STAMP = false, bool SC0 = false>
 __global__ __launch_bounds__(2 * kWave) void k_step(KParams p) {
-    __shared__ StepLds<F32, 1> sm;
+    __shared__ StepLds<WT, F32, 1> sm;
     if (threadIdx.x < kWave) run_steps<WT, HT, F32, STAMP, 1, SC0, kRoleL>(p, sm);
     else run_steps<WT, HT, F32, STAMP, 1, SC0, kRoleD>(p, sm);
 }
@@ -2191,7 +2252,7 @@ __global__ __launch_bounds__(3 * kWave) void k_rollout(KParams p) {
 // chain gains (131,072 envs: 2.8 against 4.0 us per step).
 template <int WT, int HT, bool F32, bool SC0 = false>
 __global__ __launch_bounds__(2 * kWave) void k_rollout2(KParams p) {
-    __shared__ StepLds<F32, 0> sm;
+    __shared__ StepLds<WT, F32, 0> sm;
     if (threadIdx.x < kWave) run_steps<WT, HT, F32, false, 0, SC0, kRoleL>(p, sm);
     else run_steps<WT, HT, F32, false, 0, SC0, kRoleD>(p, sm);
 }
