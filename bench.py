@@ -334,20 +334,22 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    def spawned(eng) -> int:
+    def spawned_dev(eng) -> torch.Tensor:
+        """The envs' total spawn count (every lock spawns one piece) as a
+        device scalar, computed on the current stream (no host wait)."""
         st = eng.state_tensors(("stats",), sync=False)["stats"][C.STAT["count0"]:C.STAT["count0"] + 7, :eng.n]
-        return int(st.to(torch.int64).sum().item())
+        return st.to(torch.int64).sum()
 
     def timed(eng, run, nsteps):
         """Time `run()` (enqueues exactly nsteps steps of `eng` on s): barrier +
         synchronize on both sides, max over ranks; events on s give the GPU
         span.  p_lock from the spawn counters (every lock spawns one piece),
-        read after everything enqueued before the region has finished (the
-        counters are read on the current stream; work still queued on s
-        would race them)."""
-        torch.cuda.synchronize(dev)
-        c0 = spawned(eng)
+        summed on s after everything enqueued before the region and read
+        after it (no blocking host read between the warm-up and the region:
+        a thread that just slept in a long wait issues its next launches
+        slowly, tools/k20_idle.py / k20_sync.py)."""
         with torch.cuda.stream(s):  # s is current for the whole region (graph replay launches on it)
+            c0 = spawned_dev(eng)
             ev0.record(s)  # first host calls after a stream switch are slow: not inside the region
             ev1.record(s)
             sync_all()
@@ -361,10 +363,13 @@ def main():
             sync_all()
             t4 = time.perf_counter()
         elapsed = max_over_ranks(t4 - t0)
+        with torch.cuda.stream(s):
+            c1 = spawned_dev(eng)
+        n_sp = int((c1 - c0).item())
         if DEBUG:
             print("timed: rec0 %.1f run %.1f rec1 %.1f sync %.1f us" % ((t1 - t0) * 1e6, (t2 - t1) * 1e6,
                   (t3 - t2) * 1e6, (t4 - t3) * 1e6), file=sys.stderr)
-        p_lock = (spawned(eng) - c0) / float(eng.n * nsteps)
+        p_lock = n_sp / float(eng.n * nsteps)
         return elapsed, ev0.elapsed_time(ev1), p_lock
 
     def make_actions(n, offset, gen):
@@ -443,27 +448,39 @@ def main():
             self.aptr = [ctypes.c_void_p(self.actions[t].data_ptr()) for t in range(WU + K)]
             L, ctx = self.eng._L, self.eng._ctx
             po, pr, pd = self.ptrs
+            # the ctypes argument tuple of every step, built once: the timed
+            # loop is one ctypes call per step and nothing else (return codes
+            # OR'ed, checked after the loop) -- the HIP runtime's own launch
+            # cost (~3.2 us, tools/launch_cost.hip) is then the host's whole
+            # share, under the kernel's ~4.7 us
             if f32:
-                self.launch = lambda t: C.check(L.st_step_f32(ctx, self.aptr[t], po, self.pf, pr, pd, sp))
+                self.fn = L.st_step_f32
+                self.args = [(ctx, self.aptr[t], po, self.pf, pr, pd, sp) for t in range(WU + K)]
             else:
-                self.launch = lambda t: C.check(L.st_step(ctx, self.aptr[t], po, pr, pd, sp))
+                self.fn = L.st_step
+                self.args = [(ctx, self.aptr[t], po, pr, pd, sp) for t in range(WU + K)]
+
+        def launch(self, t):
+            C.check(self.fn(*self.args[t]))
+
+        def launch_range(self, t0, t1):
+            """Steps t0 .. t1-1, one ctypes st_step call each."""
+            fn, rc = self.fn, 0
+            for a in self.args[t0:t1]:
+                rc |= fn(*a)
+            C.check(rc)
 
         def warmup(self):
             with torch.cuda.stream(s):
-                for t in range(WU):
-                    self.launch(t)
+                self.launch_range(0, WU)
             torch.cuda.synchronize(dev)
 
         def runner(self):
             if args.launch == "eager":
-                def run():
-                    for t in range(WU, WU + K):
-                        self.launch(t)
-                return run, None
+                return (lambda: self.launch_range(WU, WU + K)), None
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
-                for t in range(WU, WU + K):
-                    self.launch(t)
+                self.launch_range(WU, WU + K)
             torch.cuda.synchronize(dev)
             return g.replay, g
 
@@ -472,8 +489,13 @@ def main():
             rows reused cyclically), HIP events around them only -- the
             kernel's launch-to-launch period without the region's ramp (the
             first launch after an idle GPU, the final synchronize)."""
-            rows = list(range(WU, WU + K))
-            el, ev_ms, p_lock = timed(self.eng, lambda: [self.launch(rows[i % len(rows)]) for i in range(S)], S)
+            def run():
+                done = 0
+                while done < S:
+                    c = min(K, S - done)
+                    self.launch_range(WU, WU + c)
+                    done += c
+            el, ev_ms, p_lock = timed(self.eng, run, S)
             return ev_ms * 1e3 / S, p_lock
 
         def measure(self, steady=True):
