@@ -109,8 +109,8 @@ def kernel_source_sha() -> str:
 
 
 def step_grid(n: int) -> int:
-    """Grid size in threads of k_step / k_rollout for n envs (128 per 64 envs),
-    the key tools/pmc_summary.py files a launch under (`name@grid`)."""
+    """Grid size in threads of k_step for n envs (two waves per 64 envs),
+    part of the key tools/pmc_summary.py files a launch under."""
     return (n + 63) // 64 * 128
 
 
@@ -363,9 +363,9 @@ def main():
             sync_all()
             t4 = time.perf_counter()
         elapsed = max_over_ranks(t4 - t0)
-        with torch.cuda.stream(s):
+        with torch.cuda.stream(s):  # (the read on s too: c0 / c1 were computed there)
             c1 = spawned_dev(eng)
-        n_sp = int((c1 - c0).item())
+            n_sp = int((c1 - c0).item())
         if DEBUG:
             print("timed: rec0 %.1f run %.1f rec1 %.1f sync %.1f us" % ((t1 - t0) * 1e6, (t2 - t1) * 1e6,
                   (t3 - t2) * 1e6, (t4 - t3) * 1e6), file=sys.stderr)
@@ -378,11 +378,23 @@ def main():
             gen(t, aseed, global_offset=offset, out=a[t])
         return a
 
-    def kname_of(kind, f32, sc0):  # rocprofv3's demangled name of the 10x20 kernel
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+
+    def rollout_three_wave(n):
+        """launch_rollout's choice: the three-wave kernel up to 4 workgroups
+        (of 64 envs) per CU, else the two-wave one."""
+        return (n + 63) // 64 <= 4 * cus
+
+    def kname_of(kind, f32, sc0, n=None):  # rocprofv3's demangled name of the 10x20 kernel
         b = lambda v: "true" if v else "false"  # noqa: E731
         if kind == "step":
             return f"k_step<10, 20, {b(f32)}, false, {b(sc0)}>"
-        return f"k_rollout<10, 20, {b(f32)}, {b(sc0)}>"
+        if rollout_three_wave(n):
+            return f"k_rollout<10, 20, {b(f32)}, {b(sc0)}, false>"
+        return f"k_rollout2<10, 20, {b(f32)}, {b(sc0)}>"
+
+    def rollout_grid(n):
+        return (n + 63) // 64 * (192 if rollout_three_wave(n) else 128)
 
     def roofline(ev_us, bpe, units_per_launch, kname, extra=None, grid=None, k=1, bytes_at=None):
         """Roofline object of one launch shape: `achieved` = algorithmic bytes
@@ -598,7 +610,7 @@ def main():
                 "value": head.n_global * nch * CH / el, "ms_per_step": el / (nch * CH) * 1e3,
                 "steps_per_launch": CH, "launches": nch, "p_lock": pl,
                 "roofline": roofline(ev_us, rollout_bytes(W, H, pl, use_f32, CH), CH * n_local,
-                                     kname_of("rollout", use_f32, head.sc0), grid=step_grid(n_local), k=CH,
+                                     kname_of("rollout", use_f32, head.sc0, n_local), grid=rollout_grid(n_local), k=CH,
                                      bytes_at=lambda q, f=use_f32: rollout_bytes(W, H, q, f, CH), extra=
                                      {"bytes_formula": "rollout: I/O per step + state r/w per launch / K",
                                       "p_lock": pl})}
