@@ -586,9 +586,11 @@ def main():
             w.close()
         # K-step rollout kernel (st_rollout), continuing the headline's state:
         # a fixed CH steps per launch whatever K is (so its PMC / trace keys
-        # match the profiles' launch shape), max(1, K // CH) timed launches
+        # match the profiles' launch shape), max(5, K // CH) timed launches
+        # (at the driver's K = 20 a single launch would carry the region's
+        # fixed ~40 us alone)
         CH = args.rollout_chunk
-        nch = max(1, K // CH)
+        nch = max(5, K // CH)
         n_local = head.n_local
         ro = torch.empty((CH, W, n_local), dtype=torch.int32, device=dev)
         rr = torch.empty((CH, n_local), dtype=torch.int32, device=dev)
