@@ -392,9 +392,9 @@ __device__ __forceinline__ void mt_chunk_issue(const MtRes &rs, uint32_t mtw, bo
     // zero at the join, and the merge waits for it on the spot (before B1)
     const uint64_t m = __ballot(cand);
     c.l = m ? (int)__builtin_ctzll(m) : -1;
-    const int l = m ? c.l : 0;
-    c.pg = __shfl(pg, l);
-    c.cur = __shfl(cur, l);
+    const int l = m ? c.l : 0;  // wave-uniform: v_readlane, not an LDS permute round trip
+    c.pg = __builtin_amdgcn_readlane(pg, l);
+    c.cur = __builtin_amdgcn_readlane(cur, l);
     c.base = (uint32_t)l * (uint32_t)kMtPitch * 4u;
     const int k = c.pg + lane;
     const bool on = m != 0 && k < kMtN;
@@ -470,6 +470,53 @@ __device__ __attribute__((noinline)) void mt_finish(uint32_t *g, uint32_t *S, in
     wave_sync();
 }
 
+// The memory path of a draw: lanes still `pending` after their register
+// words read 8 words at a time from the current generation, switching to the
+// next one at index 624 (finishing it first where its chunks have not).
+// Wave-uniform.  n, kb: randint's range and getrandbits width.
+__device__ __forceinline__ void draw_slow(bool &pending, uint32_t &r, int &idx, int &pg, int &cur, uint32_t n, int kb,
+                                          uint32_t *mt_wave, uint32_t *S, int lane) {
+    if (__ballot(pending)) {
+        const MtRes rs = mt_res(mt_wave, lane);
+        do {
+            // lanes at the end of their generation switch to the next one,
+            // finishing it first where the chunks have not
+            const bool sw = pending && idx >= kMtN;
+            uint64_t fin = __ballot(sw && pg < kMtN);
+            while (fin) {
+                const int l = __builtin_ctzll(fin);
+                fin &= fin - 1;
+                mt_finish(mt_wave + (size_t)l * kMtPitch, S, lane, __shfl(pg, l), __shfl(cur, l));
+            }
+            if (sw) {
+                cur ^= 1;
+                idx = 0;
+                pg = 0;
+            }
+            const uint32_t cb = cur ? kMtB : 0u;
+            const u32x4 w0 = mt_ld16(rs, pending, cb + idx), w1 = mt_ld16(rs, pending, cb + idx + 4);
+            // both consumed here: the loop below may break before reading w1,
+            // and a load still pending at the exit makes every later write of
+            // its registers (reused by the caller) wait vmcnt(0)
+            asm volatile("" ::"v"(w0.x), "v"(w0.y), "v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w1.z),
+                         "v"(w1.w));
+            const uint32_t word[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (!__ballot(pending && idx < kMtN)) break;
+                if (pending && idx < kMtN) {
+                    const uint32_t y = mt_temper(word[j]) >> (32 - kb);
+                    ++idx;
+                    if (y < n) {
+                        pending = false;
+                        r = y;
+                    }
+                }
+            }
+        } while (__ballot(pending));
+    }
+}
+
 // _choose_shape (tetris_env.py:183-191) + the count update of _new_piece
 // (:199) for every lane with `need`: randint(1, sum(m)) = 1 + _randbelow(n)
 // with rejection sampling on getrandbits(k) (Lib/random.py:239-249).  `mtst`
@@ -543,45 +590,7 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
         }
         idx = pos;
     }
-    if (__ballot(pending)) {
-        const MtRes rs = mt_res(mt_wave, lane);
-        do {
-            // lanes at the end of their generation switch to the next one,
-            // finishing it first where the chunks have not
-            const bool sw = pending && idx >= kMtN;
-            uint64_t fin = __ballot(sw && pg < kMtN);
-            while (fin) {
-                const int l = __builtin_ctzll(fin);
-                fin &= fin - 1;
-                mt_finish(mt_wave + (size_t)l * kMtPitch, S, lane, __shfl(pg, l), __shfl(cur, l));
-            }
-            if (sw) {
-                cur ^= 1;
-                idx = 0;
-                pg = 0;
-            }
-            const uint32_t cb = cur ? kMtB : 0u;
-            const u32x4 w0 = mt_ld16(rs, pending, cb + idx), w1 = mt_ld16(rs, pending, cb + idx + 4);
-            // both consumed here: the loop below may break before reading w1,
-            // and a load still pending at the exit makes every later write of
-            // its registers (reused by the caller) wait vmcnt(0)
-            asm volatile("" ::"v"(w0.x), "v"(w0.y), "v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w1.z),
-                         "v"(w1.w));
-            const uint32_t word[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                if (!__ballot(pending && idx < kMtN)) break;
-                if (pending && idx < kMtN) {
-                    const uint32_t y = mt_temper(word[j]) >> (32 - kb);
-                    ++idx;
-                    if (y < n) {
-                        pending = false;
-                        r = y;
-                    }
-                }
-            }
-        } while (__ballot(pending));
-    }
+    draw_slow(pending, r, idx, pg, cur, n, kb, mt_wave, S, lane);
     if (need) mtst = mt_keep(mtst, mt_pack(idx, pg, cur));
     if (!need) return 0;
     int32_t rr = (int32_t)r + 1;
@@ -600,6 +609,109 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
         for (int i = 0; i < 7; ++i) cnt[i] += (i == pick);
     }
     return pick;
+}
+
+// The rollout's draw from a lane's register window (k_rollout, draw wave):
+// `wv` holds the 16 MT words at the positions from where the window was
+// loaded, of which the first `wlim` are valid (words past index 623 only if
+// the next generation was complete then) and the first `o` already consumed
+// (o may exceed 16: then none is left).  The 8 words at o.. are brought to the
+// front by a 4-stage select network (the offset differs per lane), tempered
+// as 8 independent chains, and each lane with `need` takes its first accepted
+// getrandbits(k); lanes they do not settle continue from memory (draw_slow).
+// Same rule as draw_shape (randint(1, sum(m)), tetris_env.py:183-191); `mta`
+// (idx | pg | cur) and `o` advance past the words consumed.  Wave-uniform.
+__device__ __forceinline__ int draw_win(bool need, const int32_t (&cnt)[7], uint32_t &mta, const MtPre &wv, int &o,
+                                        int wlim, uint32_t *mt_wave, uint32_t *S, int lane) {
+    int32_t maxc = cnt[0], sumc = cnt[0];
+#pragma unroll
+    for (int i = 1; i < 7; ++i) {
+        maxc = cnt[i] > maxc ? cnt[i] : maxc;
+        sumc += cnt[i];
+    }
+    const uint32_t n = (uint32_t)(35 + 7 * maxc - sumc);
+    const int kb = 32 - __builtin_clz(n);
+    int idx, pg, cur;
+    mt_unpack(mta, idx, pg, cur);
+    const uint32_t before = mta & kMtLow;
+    bool pending = need;
+    uint32_t r = 0;
+    {
+        // m ? hi : lo bitwise, one v_bitop3 (truth table 0xE4 = (a & c) | (b & ~c));
+        // a plain select here is recognised as a shifted array read and the
+        // arrays go to scratch memory
+        auto pick = [](uint32_t hi, uint32_t lo, uint32_t m) { return __builtin_amdgcn_bitop3_b32(hi, lo, m, 0xE4); };
+        // the 8 words at o.. by a 3-stage network: o < 8 (a window is
+        // reloaded after every draw, so o is the previous draw's few words;
+        // o >= 8 takes the memory path)
+        const int os = o & 7;
+        const uint32_t m4 = 0u - (uint32_t)((os >> 2) & 1), m2 = 0u - (uint32_t)((os >> 1) & 1);
+        const uint32_t m1 = 0u - (uint32_t)(os & 1);
+        uint32_t b[11], c[9], w8[8];
+#pragma unroll
+        for (int j = 0; j < 11; ++j) b[j] = pick(wv.w[j + 4], wv.w[j], m4);
+#pragma unroll
+        for (int j = 0; j < 9; ++j) c[j] = pick(b[j + 2], b[j], m2);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w8[j] = pick(c[j + 1], c[j], m1);
+        const int nv = o < 8 ? wlim - o : 0;  // valid words from o
+        // words 0-3 tempered as independent chains (acceptance >= 1/2, ~0.7
+        // typically: 4 rejections in a row are rare), 4-7 where a lane needs them
+        auto pass = [&](int j0) {
+            int first = 4;
+            uint32_t rr = 0;
+#pragma unroll
+            for (int j = 3; j >= 0; --j) {
+                const uint32_t y = mt_temper(w8[j0 + j]) >> (32 - kb);
+                const bool acc = y < n && j0 + j < nv;
+                first = acc ? j : first;
+                rr = acc ? y : rr;
+            }
+            if (pending) {
+                int pos;
+                if (first < 4) {
+                    pending = false;
+                    r = rr;
+                    pos = idx + first + 1;
+                } else {
+                    const int left = nv - j0;  // valid words this pass had
+                    pos = idx + (left < 0 ? 0 : (left < 4 ? left : 4));
+                }
+                if (pos > kMtN) {  // the draw ran into the (complete) next generation
+                    cur ^= 1;
+                    pos -= kMtN;
+                    pg = 0;
+                }
+                idx = pos;
+            }
+        };
+        pass(0);
+        if (__ballot(pending && nv > 4)) pass(4);
+    }
+    draw_slow(pending, r, idx, pg, cur, n, kb, mt_wave, S, lane);
+    if (!need) return 0;
+    mta = mt_pack(idx, pg, cur);
+    o += (int)mt_consumed(before, mta);
+    int32_t rr = (int32_t)r + 1;
+    int pick = 6;
+    bool found = false;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        rr -= 5 + maxc - cnt[i];
+        if (!found && rr <= 0) {
+            pick = i;
+            found = true;
+        }
+    }
+    return pick;
+}
+// Valid words of a window loaded at MT position m (idx | pg | cur): up to
+// index 623, or 639 when the next generation is complete (cur[624..639] is
+// next[0..15], see the layout).
+__device__ __forceinline__ int win_lim(uint32_t m) {
+    const int idx = (int)(m & 0x3FFu), pg = (int)((m >> 10) & 0x3FFu);
+    const int l = (pg == kMtN ? kMtN + kMtWin : kMtN) - idx;
+    return l < kMtWin ? l : kMtWin;
 }
 
 __device__ __forceinline__ uint32_t pack_piece(int id, int rot, int ax, int ay, int lock) {
@@ -701,6 +813,13 @@ __device__ __forceinline__ void lds_flag_set(uint32_t *f, uint32_t v) {
 __device__ __forceinline__ void lds_flag_wait(uint32_t *f, uint32_t v) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     while (__hip_atomic_load((lds_u32 *)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != v)
+        __builtin_amdgcn_s_sleep(1);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+// The same for a progress counter that the writer may have advanced past v.
+__device__ __forceinline__ void lds_flag_wait_ge(uint32_t *f, uint32_t v) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    while ((int32_t)(__hip_atomic_load((lds_u32 *)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) - v) < 0)
         __builtin_amdgcn_s_sleep(1);
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
@@ -1555,25 +1674,40 @@ __global__ __launch_bounds__(2 * kWave) void k_step(KParams p) {
 //               compaction, holes / height, scoring, death), reward / done,
 //               spawn; state in registers (piece word, clock, counters and the
 //               piece's four rotation descriptors), the board in LDS;
-//   draw   (D): the piece draw (one spawn ahead, as in st_step), its MT
-//               window in registers (reloaded for the position it commits at
-//               the end of every step, so a draw never waits for memory), the
-//               shape counts and MT word in registers, the next-generation
-//               chunk;
+//   draw   (D): the piece draws, TWO spawns ahead: each env's next two pieces
+//               (q0 = the preview of the state word, q1 = the one after it)
+//               sit in a per-lane LDS ring; a round s refills the pieces the
+//               logic wave's step s consumed.  The piece sequence does not
+//               depend on the actions (clear() keeps the shape counts,
+//               tetris_env.py:306-315; counts change only at spawns, :199),
+//               so q1 is drawn with the counts after q0's spawn, exactly the
+//               ones the reference's _choose_shape will see.  MT words come
+//               from a 16-word register window per lane (draw_win), reloaded
+//               after each draw and merged one round later, so no draw waits
+//               for memory; shape counts and MT positions in registers; the
+//               next-generation chunk;
 //   output (O): the observation of every step -- the board plane OR'ed with
 //               an overlay plane OV the logic wave writes (the current piece's
 //               cells, or for an env reset in this step its whole terminal
 //               board) -- packed and float32 stores, then OV cleared.
-// One s_barrier per step (B1: the lock mask, logic -> draw, and the pace of
-// all three); one-way LDS flags for the rest: fo (logic -> output: step t's
-// board and overlay are final), f1 (logic -> draw, deaths without
-// auto-reset), f2 (draw -> logic, the rare first draw).  The output wave
-// reads step t's planes before B1(t+1) and the logic wave modifies them only
-// after it, so the obs of step t overlaps the logic wave's action phase of
-// step t+1.  (The two-wave rollout measured 4,160 cycles per step with the
-// logic wave's chain critical -- it also painted, stored and erased the obs
-// overlay -- and the draw wave waiting 1,150 cycles for its window:
-// tools/ro_stamps.py)
+// No barrier inside the step loop: the three waves run their own chains and
+// meet only through progress counters in LDS (each written by one wave, each
+// wait one-way): fl = t + 1 once the logic wave's consumption mask of step t
+// is in cm[t & 1]; fd = s + 2 once draw round s wrote its pieces (1 after the
+// two initial draws); fo = t + 1 once step t's planes are final; fq = t + 1
+// once the output wave has read them.  The logic wave's step t needs round
+// t - 2 (fd >= t: a piece consumed at step t was drawn when the piece two
+// before it was consumed, at step <= t - 2) and the output of step t - 1
+// (fq >= t, before it changes a plane); the draw wave's round s needs fl >=
+// s + 1.  So the draw chain runs up to ~2 steps behind the logic chain and a
+// step takes the longer of the two, not their sum: round 3's B1 per step made
+// the logic wave wait ~1,400 of ~4,450 cycles for the draw wave's previous
+// step (tools/ro_stamps.py, profiles/r03/ro_stamps_3wave_fine.txt).
+// At the end, the committed state is q0's (the state word's preview and the
+// MT position after its draw); q1's draw is dropped, and st_mt_sync's rewind
+// rule is unchanged.  The next-generation chunk is built only for envs whose
+// reference state (before q0's draw) is in the generation q1 ended in, so it
+// never overwrites words a committed preview may give back.
 constexpr int kRoleO = 3;
 // issue priorities of the rollout's waves (A/B knobs)
 // (the logic wave's chain sets the step: at 3 against 0, -6% per step,
@@ -1587,12 +1721,6 @@ constexpr int kRoleO = 3;
 #ifndef ST_RO_OPRIO
 #define ST_RO_OPRIO 0
 #endif
-// the draw wave's MT windows: 1 = every lane's window reloaded at the end of
-// each step (in registers when a lane locks), 0 = loaded after B1 for the
-// locking lanes only
-#ifndef ST_RO_RWIN
-#define ST_RO_RWIN 1
-#endif
 template <int WT, bool F32>
 struct RoLds {
     static constexpr int kCols = (WT ? WT : kMaxW) + 2 * kPad;
@@ -1603,10 +1731,10 @@ struct RoLds {
     uint32_t S[kMtN];                                             // mt_finish scratch
     uint32_t O[F32 ? kWave * (kMaxW + 1) : 1];                    // float32 writer staging
     float F4[F32 ? 64 : 4] __attribute__((aligned(16)));
-    uint32_t lockm[2][2], drawm[2];
-    uint32_t pick1[kWave];
-    uint32_t mtw[2][kWave];  // the draw wave's MT word after step t (step-parity double buffer)
-    uint32_t f1, f2, fo;
+    uint32_t qring[kWave];  // per lane: the env's i-th queued piece in bits 4 (i & 3) .. (draw -> logic)
+    uint32_t cm[2][2];      // step t's consumption mask (a spawn or a same-step reset) in cm[t & 1]
+    uint32_t act[4][kWave];  // step t's actions in act[t & 3] (draw -> logic, four steps ahead)
+    uint32_t fl, fd, fo, fq;  // progress counters (see above)
 };
 
 // d[r] by selects on values (a select between two array elements would be
@@ -1732,8 +1860,9 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
 #pragma unroll
         for (int q = 2; q < kHotQ; ++q) *reinterpret_cast<uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]) = sv[q - 2];
         if (lane == 0) {
-            sm.f1 = 0u;
-            sm.f2 = 0u;
+            sm.fl = 0u;
+            sm.fd = 0u;
+            sm.fq = 0u;
         }
     } else {
         for (int i = lane; i < RoLds<WT, F32>::kCols * kWave; i += kWave) OV[i] = 0u;
@@ -1750,16 +1879,21 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
         int32_t score = (int32_t)ss(ST_STAT_SCORE), lines = (int32_t)ss(ST_STAT_LINES);
         int32_t holes = (int32_t)ss(ST_STAT_HOLES), height = (int32_t)ss(ST_STAT_PIECE_HEIGHT);
         int32_t deaths = (int32_t)ss(ST_STAT_DEATHS);
-        uint32_t mt0 = ss(ST_STAT_MT_INDEX);  // the preview bits of the draw wave's word
-        uint2 d4[4];                          // the current piece's four rotations
+        uint2 d4[4];  // the current piece's four rotations
 #pragma unroll
         for (int r = 0; r < 4; ++r) d4[r] = tab((int)(pw & 7u) * 4 + r);
-        uint32_t act_next = p.actions[real ? e : p.n - 1];
         bool bad_act = false;
+        uint32_t nq = 0;  // pieces this env consumed so far (its next spawn: ring slot nq & 3)
         for (int t = 0; t < K; ++t) {
-            const uint32_t act = real ? act_next : 6u;
+            // the action, from the ring the draw wave fills four steps ahead
+            // (at the end of round t - 4, or its initial loads for t < 4),
+            // published by round t - 3's fd: an LDS read, no
+            // memory wait on this chain (CDNA counts loads and stores in one
+            // in-order vmcnt: a load here waited for the previous step's
+            // reward / done / counter stores as well)
+            lds_flag_wait_ge(&sm.fd, t > 2 ? (uint32_t)t - 1u : 1u);
+            const uint32_t act = real ? sm.act[t & 3][lane] : 6u;
             bad_act |= act > 6u;
-            if (t + 1 < K) act_next = p.actions[(int64_t)(t + 1) * p.n + (real ? e : p.n - 1)];
             int rot = (int)((pw >> 3) & 3u);
             int ax = (int)((pw >> 5) & 63u);
             int ay = (int)((pw >> 11) & 63u);
@@ -1805,21 +1939,17 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 locknow = lock == 0 && !(kAblate & 1u);
             }
             stamp(2);
-            {
-                const uint64_t m = __ballot(locknow);
-                if (lane == 0) {
-                    sm.lockm[t & 1][0] = (uint32_t)m;
-                    sm.lockm[t & 1][1] = (uint32_t)(m >> 32);
-                }
-            }
-            wg_barrier();  // B1
-            stamp(3);
-            if (t > 0) mt0 = sm.mtw[(t - 1) & 1][lane];  // the draw wave's word after step t-1
-            // the preview's descriptors, for a spawn below (read under the lock path)
+            // the next spawn's piece (drawn by round t - 2 at the latest; the
+            // two initial draws count as one round) and its descriptors, for a
+            // spawn below (read under the lock path); then the output wave's
+            // reads of step t - 1's planes, before this step changes them
+            if (!(kAblate & 32u)) lds_flag_wait_ge(&sm.fd, t > 1 ? (uint32_t)t : 1u);
+            const int sid = (int)((sm.qring[lane] >> (4u * (nq & 3u))) & 7u);
             uint2 s4[4];
-            const int pvid = pv_ok(mt0) ? pv_id(mt0) : 0;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) s4[r] = tab(pvid * 4 + r);
+            for (int r = 0; r < 4; ++r) s4[r] = tab(sid * 4 + r);
+            if (!(kAblate & 32u)) lds_flag_wait_ge(&sm.fq, (uint32_t)t);
+            stamp(3);
 
             // ---- lock path (tetris_env.py:263-299) ----
             bool died = false, spawn = false;
@@ -1923,35 +2053,23 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             }
             stamp(4);
             const bool reset_now = died && p.autoreset == ST_AUTORESET_SAME_STEP;
-            const bool draw = spawn || reset_now;  // the lock consumed the preview
-            if (p.autoreset != ST_AUTORESET_SAME_STEP) {  // deaths keep the preview: tell the draw wave
+            // the lock consumed the queue's head (a death without auto-reset
+            // keeps it for the next st_reset)
+            const bool draw = spawn || reset_now;
+            {
                 const uint64_t m = __ballot(draw);
                 if (lane == 0) {
-                    sm.drawm[0] = (uint32_t)m;
-                    sm.drawm[1] = (uint32_t)(m >> 32);
-                    lds_flag_set(&sm.f1, (uint32_t)t + 1u);
+                    sm.cm[t & 1][0] = (uint32_t)m;
+                    sm.cm[t & 1][1] = (uint32_t)(m >> 32);
+                    lds_flag_set(&sm.fl, (uint32_t)t + 1u);
                 }
             }
+            nq += draw ? 1u : 0u;
             {
                 const auto rr = buf_rsrc(p.reward ? p.reward + (int64_t)t * p.n : nullptr, (uint32_t)p.n * 4u);
                 const auto rd = buf_rsrc(p.done ? p.done + (int64_t)t * p.n : nullptr, (uint32_t)p.n);
                 __builtin_amdgcn_raw_buffer_store_b32(rew, rr, real ? (uint32_t)e * 4u : kOff, 0, 0);
                 __builtin_amdgcn_raw_buffer_store_b8((char)(died ? 1 : 0), rd, real ? (uint32_t)e : kOff, 0, 0);
-            }
-            // spawn id: the preview; a lane without one takes the draw wave's first draw (rare)
-            int sid = pvid;
-            {
-                const bool need1 = draw && !pv_ok(mt0);
-                if (__ballot(need1)) {
-                    lds_flag_wait(&sm.f2, (uint32_t)t + 1u);
-                    if (need1) sid = (int)sm.pick1[lane];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const uint2 v = tab(sid * 4 + r);
-                        s4[r].x = need1 ? v.x : s4[r].x;
-                        s4[r].y = need1 ? v.y : s4[r].y;
-                    }
-                }
             }
             stamp(5);
             // ---- this step's obs (tetris_env.py:301-302) for the output wave ----
@@ -2033,108 +2151,144 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
         }
     } else if constexpr (ROLE == kRoleD) {
         // ================================================================ draw
-        const MtRes mrs = mt_res(p.mt + e0 * kMtPitch, lane);
-        uint32_t mtw_r = ss(ST_STAT_MT_INDEX);
-        int32_t cnt_r[7];
+        uint32_t *const mtg = p.mt + e0 * kMtPitch;
+        const MtRes mrs = mt_res(mtg, lane);
+        const uint32_t w0 = ss(ST_STAT_MT_INDEX);
+        int32_t cnt_r[7];  // shape_counts (the spawned pieces only)
 #pragma unroll
         for (int i = 0; i < 7; ++i) cnt_r[i] = (int32_t)ss(ST_STAT_COUNT0 + i);
-        MtPre win;
-        int win_pg = -1;
-        if constexpr (ST_RO_RWIN) {
-            mt_pre_load<kMtWin>(mrs, mtw_r, real, win);
-            win_pg = (int)((mtw_r >> 10) & 0x3FFu);
+        // mtc: the committed state word (the queue head q0 as its preview, the
+        // MT position after q0's draw); mta: the MT position after the last
+        // queued draw (q1's), c1 the words that draw consumed
+        uint32_t mtc = w0, mta = w0 & kMtLow, c1 = 0;
+        // the register window: words from where it was loaded, o consumed,
+        // wlim valid; wn: the next window, loaded after a lane's draw and
+        // merged at the end of the following round (o_rl: o at its load)
+        // the logic wave's actions, four steps ahead: loaded at the start of
+        // round s, written at its end (after the window merge, which waits
+        // for the loads issued before them anyway), published by round s +
+        // 1's fd (no branch around a load: steps >= K read nothing)
+        auto act_at = [&](int t) -> uint32_t {
+            const bool in = t < K;  // wave-uniform (a per-lane resource base makes a waterfall loop)
+            return __builtin_amdgcn_raw_buffer_load_b8(buf_rsrc(p.actions + (int64_t)(in ? t : 0) * p.n, (uint32_t)p.n),
+                                                       in && real ? (uint32_t)e : kOff, 0, 0);
+        };
+        const uint32_t a0 = act_at(0), a1 = act_at(1), a2 = act_at(2), a3 = act_at(3);
+        MtPre win, wn = {};
+        int o = 0, wlim = win_lim(mta), o_rl = 0, wlim_n = 0;
+        mt_pre_load<kMtWin>(mrs, mta, real, win);
+        mt_win_consume<kMtWin>(win);
+        int q0 = pv_id(w0), q1;
+        {
+            // the queue's two pieces: q0 where the state has no preview
+            // (st_seed / st_mt_sync / a host-written state), then q1 with the
+            // counts after q0's spawn
+            const bool need1 = real && !pv_ok(w0);
+            if (__ballot(need1)) {
+                const int pk = draw_win(need1, cnt_r, mta, win, o, wlim, mtg, sm.S, lane);
+                if (need1) q0 = pk;
+            }
+            int32_t cq[7];
+#pragma unroll
+            for (int i = 0; i < 7; ++i) cq[i] = cnt_r[i] + (i == q0);
+            const uint32_t m0 = mta;
+            q1 = draw_win(real, cq, mta, win, o, wlim, mtg, sm.S, lane);
+            c1 = mt_consumed(m0, mta);
         }
-        for (int t = 0; t < K; ++t) {
-            const uint32_t mt0 = mtw_r;
+        uint32_t qw = (uint32_t)q0 | ((uint32_t)q1 << 4), nd = 2;  // the ring word, pieces drawn
+        sm.qring[lane] = qw;
+        sm.act[0][lane] = a0;
+        sm.act[1][lane] = a1;
+        sm.act[2][lane] = a2;
+        sm.act[3][lane] = a3;
+        if (lane == 0) lds_flag_set(&sm.fd, 1u);
+        if constexpr (ST_RO_DPRIO > 0) __builtin_amdgcn_s_setprio(ST_RO_DPRIO);
+        bool rl = false;  // wn holds a reload to merge
+        for (int s = 0; s < K; ++s) {
             stamp(1);
-            // this step's next-generation chunk: operands issued before B1
+            // this round's next-generation chunk, for an env whose reference
+            // state (before q0's draw; q0's draw straddled index 624 when idx
+            // <= c) lies in the generation mta is in: operands issued first
+            const uint32_t an = act_at(s + 4);
             MtChunk chunk;
-            mt_chunk_issue(mrs, mt0, real && !(kAblate & 2u), lane, chunk);
-            stamp(2);
-            wg_barrier();  // B1
-            stamp(3);
-            if constexpr (ST_RO_DPRIO > 0) __builtin_amdgcn_s_setprio(ST_RO_DPRIO);
-            bool locknow;
             {
-                const uint32_t w = lane < 32 ? sm.lockm[t & 1][0] : sm.lockm[t & 1][1];
-                locknow = (w >> (lane & 31)) & 1u;
+                int ic, pgc, cc;
+                mt_unpack(mtc, ic, pgc, cc);
+                const int ref = cc ^ (pv_ok(mtc) && ic <= (int)((mtc >> 25) & kPvCMax) ? 1 : 0);
+                mt_chunk_issue(mrs, mta, real && ref == (int)((mta >> 20) & 1u) && !(kAblate & 16u), lane, chunk);
             }
-            // every locking lane draws (speculatively: a death without
-            // auto-reset keeps its preview, committed below only where the
-            // lock consumed it): the first draw where there is no preview
-            // (rare), then the next preview
-            uint32_t mtst = mt0;
-            int sid = pv_id(mt0);
-            int32_t cnt[7];
+            lds_flag_wait_ge(&sm.fl, (uint32_t)s + 1u);
+            stamp(2);
+            bool cons;
+            {
+                const uint32_t w = lane < 32 ? sm.cm[s & 1][0] : sm.cm[s & 1][1];
+                cons = real && ((w >> (lane & 31)) & 1u) && !(kAblate & 2u);
+            }
+            // step s consumed q0: count it (_new_piece :199), commit q1 as the
+            // preview, draw the piece after it
 #pragma unroll
-            for (int i = 0; i < 7; ++i) cnt[i] = cnt_r[i];
-            if constexpr (STAMP) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                stamp(4);
+            for (int i = 0; i < 7; ++i) cnt_r[i] += (cons && i == q0);
+            if (cons) {
+                mtc = pv_pack(mta, q1, c1);
+                q0 = q1;
             }
-            uint32_t mt_new = mtst;
-            if constexpr (!ST_RO_RWIN) mt_pre_load<kMtWin>(mrs, mt0, locknow, win);  // locking lanes, after B1
-            if (!(kAblate & 2u)) {
-                mt_win_consume<kMtWin>(win);
-                const bool need1 = locknow && !pv_ok(mt0);
-                if (__ballot(need1)) {  // after st_seed / st_mt_sync / a host-written state
-                    const int pk = draw_shape<kMtWin, false>(need1, cnt, mtst, p.mt + e0 * kMtPitch, sm.S, lane,
-                                                             win, false);
-                    if (need1) sid = pk;
-                }
-                sm.pick1[lane] = (uint32_t)sid;
-                if (lane == 0) lds_flag_set(&sm.f2, (uint32_t)t + 1u);
+            int32_t cq[7];
 #pragma unroll
-                for (int i = 0; i < 7; ++i) cnt[i] += (locknow && i == sid);  // _new_piece :199
-                const uint32_t m0 = mtst;
-                const int npv = draw_shape<kMtWin, false>(locknow, cnt, mtst, p.mt + e0 * kMtPitch, sm.S, lane, win,
-                                                          locknow && pv_ok(mt0), win_pg);
-                mt_new = pv_pack(mtst, npv, mt_consumed(m0, mtst));
-            } else {
-                sm.pick1[lane] = (uint32_t)sid;
-                if (lane == 0) lds_flag_set(&sm.f2, (uint32_t)t + 1u);
+            for (int i = 0; i < 7; ++i) cq[i] = cnt_r[i] + (i == q0);
+            const uint32_t m0 = mta;
+            const int pk = draw_win(cons, cq, mta, win, o, wlim, mtg, sm.S, lane);
+            if (cons) {
+                q1 = pk;
+                c1 = mt_consumed(m0, mta);
+                const uint32_t sh = 4u * (nd & 3u);
+                qw = (qw & ~(0xFu << sh)) | ((uint32_t)pk << sh);
+                nd += 1u;
             }
+            sm.qring[lane] = qw;
+            if (lane == 0) lds_flag_set(&sm.fd, (uint32_t)s + 2u);
+            stamp(3);
             const int chunk_pg = mt_chunk_store<0>(mrs, lane, chunk);
-            const bool chunk_me = lane == chunk.l;
-            stamp(5);
-            bool dr = locknow;
-            if (p.autoreset != ST_AUTORESET_SAME_STEP) {
-                lds_flag_wait(&sm.f1, (uint32_t)t + 1u);
-                const uint32_t w = lane < 32 ? sm.drawm[0] : sm.drawm[1];
-                dr = (w >> (lane & 31)) & 1u;
-            }
-            uint32_t mt_out = dr ? mt_new : mt0;
-            if (chunk_me && (mt_out & (1u << 20)) == (mt0 & (1u << 20))) {
-                int i2, pg2, c2;
-                mt_unpack(mt_out, i2, pg2, c2);
-                mt_out = mt_keep(mt_out, mt_pack(i2, chunk_pg, c2));
-            }
-            sm.mtw[t & 1][lane] = mt_out;  // the logic wave reads it after B1(t + 1)
+            // windows: merge the reload of the previous round, reload where
+            // this round drew (valid words by the progress before this
+            // round's chunk: conservative)
+            mt_win_consume<kMtWin>(wn);
+            if (rl) {
 #pragma unroll
-            for (int i = 0; i < 7; ++i) cnt_r[i] += (dr && i == sid);  // shape_counts[name] += 1, :199
-            mtw_r = mt_out;
-            // next step's windows: the last memory operations of this step
-            // (the progress of before this step's chunk: conservative)
-            if constexpr (ST_RO_RWIN) {
-                mt_pre_load<kMtWin>(mrs, mt_out, real, win);
-                win_pg = (int)((mt0 >> 10) & 0x3FFu);
+                for (int j = 0; j < kMtWin; ++j) win.w[j] = wn.w[j];
+                o -= o_rl;
+                wlim = wlim_n;
             }
-            stamp(6);
+            rl = cons;
+            sm.act[s & 3][lane] = an;  // step s + 4's (the logic wave has read step s's)
+            mt_pre_load<kMtWin>(mrs, mta, rl, wn);
+            o_rl = o;
+            wlim_n = win_lim(mta);
+            if (lane == chunk.l && ((mta ^ m0) & (1u << 20)) == 0u) {
+                int i2, pg2, c2;
+                mt_unpack(mta, i2, pg2, c2);
+                mta = mt_pack(i2, chunk_pg, c2);
+            }
+            stamp(4);
         }
         wg_barrier();
+        // the committed word's next-generation progress: mta's where both are
+        // in one generation, else complete (mta's generation is mtc's next)
+        {
+            int ic, pgc, cc, ia, pga, ca;
+            mt_unpack(mtc, ic, pgc, cc);
+            mt_unpack(mta, ia, pga, ca);
+            mtc = mt_keep(mtc, mt_pack(ic, cc == ca ? pga : kMtN, cc));
+        }
 #pragma unroll
         for (int i = 0; i < 7; ++i) ss(ST_STAT_COUNT0 + i) = (uint32_t)cnt_r[i];
-        ss(ST_STAT_MT_INDEX) = mtw_r;
+        ss(ST_STAT_MT_INDEX) = mtc;
         wave_sync();
     } else {
         // ================================================================ output
         const bool wide_obs = (p.n & 3) == 0 && e0 + kWave <= p.n && (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0;
         for (int t = 0; t < K; ++t) {
+            lds_flag_wait_ge(&sm.fo, (uint32_t)t + 1u);
             stamp(1);
-            wg_barrier();  // B1 (keeps the pace; the planes of step t-1 were read before it)
-            stamp(2);
-            lds_flag_wait(&sm.fo, (uint32_t)t + 1u);
-            stamp(3);
             uint32_t *const obs_t = p.obs ? p.obs + (int64_t)t * W * p.n : nullptr;
             if (obs_t && !(kAblate & 8u)) {
                 if (wide_obs) {
@@ -2205,7 +2359,8 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             for (int q = 0; q < NBQ; ++q)
                 if ((WT || 4 * q < W) && 4 * q + lrow < W)
                     *reinterpret_cast<uint4 *>(&OV[(4 * q + lrow + kPad) * kWave + lcc]) = make_uint4(0u, 0u, 0u, 0u);
-            stamp(4);
+            if (lane == 0) lds_flag_set(&sm.fq, (uint32_t)t + 1u);  // the logic wave may change the planes
+            stamp(2);
         }
         wg_barrier();
     }

@@ -29,11 +29,11 @@ buf = np.zeros(nw * W, np.uint64)
 acts = torch.stack([b.gen_actions(t, 0x5EED).clone() for t in range(CH * NL)])
 out = {}
 # phases in execution order, by the stamp index that ends them
-LOGIC = [(1, "step start (action load)"), (2, "action + drop"), (3, "ballot + B1 wait"),
-         (4, "lock path"), (5, "reward/done + spawn id"), (6, "obs planes + state")]
-DRAW = [(1, "step start"), (2, "chunk issue"), (3, "B1 wait"), (4, "MT window wait"),
-        (5, "draws + chunk store"), (6, "commit + window reload")]
-OUT = [(1, "step start"), (2, "B1 wait"), (3, "wait for the planes"), (4, "obs stores + clear")]
+LOGIC = [(1, "step start (action load)"), (2, "action + drop"), (3, "queue / planes wait"),
+         (4, "lock path"), (5, "reward/done + mask"), (6, "obs planes + state")]
+DRAW = [(1, "round start"), (2, "chunk issue + mask wait"), (3, "draw + ring"),
+        (4, "chunk store + windows")]
+OUT = [(1, "wait for the planes"), (2, "obs stores + clear")]
 res = []
 for c in range(NL):
     b.rollout(acts[c * CH:(c + 1) * CH], obs="packed", out=out)
