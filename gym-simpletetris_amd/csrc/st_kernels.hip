@@ -692,16 +692,14 @@ __device__ __forceinline__ int draw_win(bool need, const int32_t (&cnt)[7], uint
     if (!need) return 0;
     mta = mt_pack(idx, pg, cur);
     o += (int)mt_consumed(before, mta);
-    int32_t rr = (int32_t)r + 1;
-    int pick = 6;
-    bool found = false;
+    // the first i with r + 1 <= m_0 + .. + m_i (m_i = 5 + maxc - cnt[i],
+    // :186-191) = the number of prefix sums below r + 1: independent
+    // compares, no serial "found" chain
+    int pick = 0, sum = 0;
 #pragma unroll
-    for (int i = 0; i < 7; ++i) {
-        rr -= 5 + maxc - cnt[i];
-        if (!found && rr <= 0) {
-            pick = i;
-            found = true;
-        }
+    for (int i = 0; i < 6; ++i) {
+        sum += 5 + maxc - cnt[i];
+        pick += sum <= (int)r ? 1 : 0;
     }
     return pick;
 }
