@@ -383,11 +383,8 @@ struct MtChunk {
     int l;          // chosen lane (-1: none)
     int pg, cur;    // its progress and current buffer
 };
-__device__ __forceinline__ void mt_chunk_issue(const MtRes &rs, uint32_t mtw, bool real, int lane, MtChunk &c) {
-    int idx, pg, cur;
-    mt_unpack(mtw, idx, pg, cur);
-    const int cc = (int)((mtw >> 25) & kPvCMax);
-    const bool cand = real && pg < kMtN && !(pv_ok(mtw) && idx <= cc);
+// (cand, pg, cur: per lane; the chosen lane's progress and current buffer)
+__device__ __forceinline__ void mt_chunk_issue_pc(const MtRes &rs, bool cand, int pg, int cur, int lane, MtChunk &c) {
     // branch-free: a load issued on one path only would be merged with a
     // zero at the join, and the merge waits for it on the spot (before B1)
     const uint64_t m = __ballot(cand);
@@ -403,6 +400,12 @@ __device__ __forceinline__ void mt_chunk_issue(const MtRes &rs, uint32_t mtw, bo
     c.a0 = __builtin_amdgcn_raw_buffer_load_b32(rs.r, on ? c.base + 4u * (cb + (uint32_t)k) : kOff, 0, 0);
     c.a1 = __builtin_amdgcn_raw_buffer_load_b32(rs.r, on ? c.base + 4u * (cb + (uint32_t)k + 1u) : kOff, 0, 0);
     c.x = __builtin_amdgcn_raw_buffer_load_b32(rs.r, on ? c.base + 4u * xo : kOff, 0, 0);
+}
+__device__ __forceinline__ void mt_chunk_issue(const MtRes &rs, uint32_t mtw, bool real, int lane, MtChunk &c) {
+    int idx, pg, cur;
+    mt_unpack(mtw, idx, pg, cur);
+    const int cc = (int)((mtw >> 25) & kPvCMax);
+    mt_chunk_issue_pc(rs, real && pg < kMtN && !(pv_ok(mtw) && idx <= cc), pg, cur, lane, c);
 }
 // Compute and store the chunk (+ the pad copy of next[0..15] when next = A);
 // returns the chosen env's new progress.  AUX: kNT in st_step; plain in
@@ -474,6 +477,11 @@ __device__ __attribute__((noinline)) void mt_finish(uint32_t *g, uint32_t *S, in
 // words read 8 words at a time from the current generation, switching to the
 // next one at index 624 (finishing it first where its chunks have not).
 // Wave-uniform.  n, kb: randint's range and getrandbits width.
+// FIN_ALL: a successor is finished from word 0 (the rollout whose output
+// wave builds the chunks: their stores may still be in flight when it
+// publishes the progress, so the progress is not trusted here; the words it
+// rewrites are the same values)
+template <bool FIN_ALL = false>
 __device__ __forceinline__ void draw_slow(bool &pending, uint32_t &r, int &idx, int &pg, int &cur, uint32_t n, int kb,
                                           uint32_t *mt_wave, uint32_t *S, int lane) {
     if (__ballot(pending)) {
@@ -486,7 +494,7 @@ __device__ __forceinline__ void draw_slow(bool &pending, uint32_t &r, int &idx, 
             while (fin) {
                 const int l = __builtin_ctzll(fin);
                 fin &= fin - 1;
-                mt_finish(mt_wave + (size_t)l * kMtPitch, S, lane, __shfl(pg, l), __shfl(cur, l));
+                mt_finish(mt_wave + (size_t)l * kMtPitch, S, lane, FIN_ALL ? 0 : __shfl(pg, l), __shfl(cur, l));
             }
             if (sw) {
                 cur ^= 1;
@@ -621,6 +629,7 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
 // getrandbits(k); lanes they do not settle continue from memory (draw_slow).
 // Same rule as draw_shape (randint(1, sum(m)), tetris_env.py:183-191); `mta`
 // (idx | pg | cur) and `o` advance past the words consumed.  Wave-uniform.
+template <bool FIN_ALL>
 __device__ __forceinline__ int draw_win(bool need, const int32_t (&cnt)[7], uint32_t &mta, const MtPre &wv, int &o,
                                         int wlim, uint32_t *mt_wave, uint32_t *S, int lane) {
     int32_t maxc = cnt[0], sumc = cnt[0];
@@ -688,7 +697,7 @@ __device__ __forceinline__ int draw_win(bool need, const int32_t (&cnt)[7], uint
         pass(0);
         if (__ballot(pending && nv > 4)) pass(4);
     }
-    draw_slow(pending, r, idx, pg, cur, n, kb, mt_wave, S, lane);
+    draw_slow<FIN_ALL>(pending, r, idx, pg, cur, n, kb, mt_wave, S, lane);
     if (!need) return 0;
     mta = mt_pack(idx, pg, cur);
     o += (int)mt_consumed(before, mta);
@@ -1719,6 +1728,9 @@ constexpr int kRoleO = 3;
 #ifndef ST_RO_OPRIO
 #define ST_RO_OPRIO 0
 #endif
+#ifndef ST_RO_CHO
+#define ST_RO_CHO 1
+#endif
 template <int WT, bool F32>
 struct RoLds {
     static constexpr int kCols = (WT ? WT : kMaxW) + 2 * kPad;
@@ -1732,6 +1744,9 @@ struct RoLds {
     uint32_t qring[kWave];  // per lane: the env's i-th queued piece in bits 4 (i & 3) .. (draw -> logic)
     uint32_t cm[2][2];      // step t's consumption mask (a spawn or a same-step reset) in cm[t & 1]
     uint32_t act[4][kWave];  // step t's actions in act[t & 3] (draw -> logic, four steps ahead)
+    // packed obs (the output wave builds the next-generation chunks):
+    uint32_t cw[kWave];   // per lane: chunk candidate << 31 | cur << 10 | pg (draw -> output)
+    uint32_t cpg[kWave];  // per lane: valid << 31 | cur << 10 | pg after a chunk (output -> draw)
     uint32_t fl, fd, fo, fq;  // progress counters (see above)
 };
 
@@ -1747,6 +1762,10 @@ __device__ __forceinline__ uint2 sel4(const uint2 (&d)[4], int r) {
 template <int WT, int HT, bool F32, bool SC0, bool STAMP, int ROLE>
 __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &sm) {
     constexpr bool S32 = HT != 0 && HT <= 25;  // see pc_bits
+    // the next-generation chunks: built by the output wave with packed obs
+    // (it idles most of a step), by the draw wave with float32 obs (the
+    // output wave's stores set that step)
+    constexpr bool CHO = !F32 && ST_RO_CHO;
     const uint32_t kFlags = SC0 ? (p.flags & (ST_REWARD_STEP | ST_STEP_RESET)) : p.flags;
 #if defined(ST_ABLATION) && ST_ABLATION
     const uint32_t kAblate = p.ablate;
@@ -1862,8 +1881,10 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             sm.fd = 0u;
             sm.fq = 0u;
         }
+        sm.cw[lane] = 0u;
     } else {
         for (int i = lane; i < RoLds<WT, F32>::kCols * kWave; i += kWave) OV[i] = 0u;
+        sm.cpg[lane] = 0u;
     }
     wg_barrier();  // B0
     stamp(0);
@@ -2183,14 +2204,14 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             // counts after q0's spawn
             const bool need1 = real && !pv_ok(w0);
             if (__ballot(need1)) {
-                const int pk = draw_win(need1, cnt_r, mta, win, o, wlim, mtg, sm.S, lane);
+                const int pk = draw_win<CHO>(need1, cnt_r, mta, win, o, wlim, mtg, sm.S, lane);
                 if (need1) q0 = pk;
             }
             int32_t cq[7];
 #pragma unroll
             for (int i = 0; i < 7; ++i) cq[i] = cnt_r[i] + (i == q0);
             const uint32_t m0 = mta;
-            q1 = draw_win(real, cq, mta, win, o, wlim, mtg, sm.S, lane);
+            q1 = draw_win<CHO>(real, cq, mta, win, o, wlim, mtg, sm.S, lane);
             c1 = mt_consumed(m0, mta);
         }
         uint32_t qw = (uint32_t)q0 | ((uint32_t)q1 << 4), nd = 2;  // the ring word, pieces drawn
@@ -2208,12 +2229,25 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             // state (before q0's draw; q0's draw straddled index 624 when idx
             // <= c) lies in the generation mta is in: operands issued first
             const uint32_t an = act_at(s + 4);
-            MtChunk chunk;
-            {
+            // the env's reference generation (the state before q0's draw;
+            // q0's draw straddled index 624 when idx <= c)
+            auto ref_cur = [&]() {
                 int ic, pgc, cc;
                 mt_unpack(mtc, ic, pgc, cc);
-                const int ref = cc ^ (pv_ok(mtc) && ic <= (int)((mtc >> 25) & kPvCMax) ? 1 : 0);
-                mt_chunk_issue(mrs, mta, real && ref == (int)((mta >> 20) & 1u) && !(kAblate & 16u), lane, chunk);
+                return cc ^ (pv_ok(mtc) && ic <= (int)((mtc >> 25) & kPvCMax) ? 1 : 0);
+            };
+            [[maybe_unused]] MtChunk chunk;
+            if constexpr (CHO) {
+                // the output wave's finished chunks: the progress, where the
+                // generation is still the one the chunk was built for
+                const uint32_t v = sm.cpg[lane];
+                int ia, pga, ca;
+                mt_unpack(mta, ia, pga, ca);
+                if ((v >> 31) && (int)((v >> 10) & 1u) == ca && (int)(v & 0x3FFu) > pga)
+                    mta = mt_pack(ia, (int)(v & 0x3FFu), ca);
+            } else {
+                mt_chunk_issue(mrs, mta, real && ref_cur() == (int)((mta >> 20) & 1u) && !(kAblate & 16u), lane,
+                               chunk);
             }
             lds_flag_wait_ge(&sm.fl, (uint32_t)s + 1u);
             stamp(2);
@@ -2234,7 +2268,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
 #pragma unroll
             for (int i = 0; i < 7; ++i) cq[i] = cnt_r[i] + (i == q0);
             const uint32_t m0 = mta;
-            const int pk = draw_win(cons, cq, mta, win, o, wlim, mtg, sm.S, lane);
+            const int pk = draw_win<CHO>(cons, cq, mta, win, o, wlim, mtg, sm.S, lane);
             if (cons) {
                 q1 = pk;
                 c1 = mt_consumed(m0, mta);
@@ -2245,7 +2279,18 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             sm.qring[lane] = qw;
             if (lane == 0) lds_flag_set(&sm.fd, (uint32_t)s + 2u);
             stamp(3);
-            const int chunk_pg = mt_chunk_store<0>(mrs, lane, chunk);
+            [[maybe_unused]] int chunk_pg = 0;
+            if constexpr (CHO) {
+                // this env's chunk candidacy for the output wave: the
+                // reference state in the generation mta is in, successor
+                // incomplete
+                int ia, pga, ca;
+                mt_unpack(mta, ia, pga, ca);
+                const bool cand = real && ref_cur() == ca && pga < kMtN && !(kAblate & 16u);
+                sm.cw[lane] = (cand ? 0x80000000u : 0u) | ((uint32_t)ca << 10) | (uint32_t)pga;
+            } else {
+                chunk_pg = mt_chunk_store<0>(mrs, lane, chunk);
+            }
             // windows: merge the reload of the previous round, reload where
             // this round drew (valid words by the progress before this
             // round's chunk: conservative)
@@ -2261,14 +2306,23 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             mt_pre_load<kMtWin>(mrs, mta, rl, wn);
             o_rl = o;
             wlim_n = win_lim(mta);
-            if (lane == chunk.l && ((mta ^ m0) & (1u << 20)) == 0u) {
-                int i2, pg2, c2;
-                mt_unpack(mta, i2, pg2, c2);
-                mta = mt_pack(i2, chunk_pg, c2);
+            if constexpr (!CHO) {
+                if (lane == chunk.l && ((mta ^ m0) & (1u << 20)) == 0u) {
+                    int i2, pg2, c2;
+                    mt_unpack(mta, i2, pg2, c2);
+                    mta = mt_pack(i2, chunk_pg, c2);
+                }
             }
             stamp(4);
         }
         wg_barrier();
+        if constexpr (CHO) {  // the output wave's last chunks (stored and published before the barrier)
+            const uint32_t v = sm.cpg[lane];
+            int ia, pga, ca;
+            mt_unpack(mta, ia, pga, ca);
+            if ((v >> 31) && (int)((v >> 10) & 1u) == ca && (int)(v & 0x3FFu) > pga)
+                mta = mt_pack(ia, (int)(v & 0x3FFu), ca);
+        }
         // the committed word's next-generation progress: mta's where both are
         // in one generation, else complete (mta's generation is mtc's next)
         {
@@ -2284,8 +2338,32 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
     } else {
         // ================================================================ output
         const bool wide_obs = (p.n & 3) == 0 && e0 + kWave <= p.n && (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0;
+        // packed obs: this wave builds the next-generation chunks (it idles
+        // most of each step), one per step, for the lowest lane the draw
+        // wave's cw word names; the new progress is published (cpg) right
+        // after the chunk's stores are issued, and the wave's own last chunk
+        // overrides a cw that does not show it yet.  A draw reads words past
+        // index 623 only once the whole successor is published, 9+ chunks
+        // after next[0..15] were stored (and each later chunk's operand
+        // loads waited for those stores: one in-order vmcnt); the draw wave's
+        // cooperative finish (mt_finish) rebuilds a successor from word 0,
+        // not trusting the progress (MT words are deterministic: a chunk
+        // racing it writes the same values).
+        [[maybe_unused]] const MtRes orm = mt_res(p.mt + e0 * kMtPitch, lane);
+        [[maybe_unused]] int last_l = -1, last_cur = 0, last_pg = 0;
         for (int t = 0; t < K; ++t) {
             lds_flag_wait_ge(&sm.fo, (uint32_t)t + 1u);
+            // the chunk's operands, issued before the obs stores (their
+            // latency overlaps them, and the wait for them does not wait for
+            // the stores: one in-order vmcnt)
+            [[maybe_unused]] MtChunk ch;
+            if constexpr (CHO) {
+                const uint32_t w = sm.cw[lane];
+                int pg = (int)(w & 0x3FFu);
+                const int cur = (int)((w >> 10) & 1u);
+                if (lane == last_l && cur == last_cur && last_pg > pg) pg = last_pg;
+                mt_chunk_issue_pc(orm, (w >> 31) != 0u && pg < kMtN, pg, cur, lane, ch);
+            }
             stamp(1);
             uint32_t *const obs_t = p.obs ? p.obs + (int64_t)t * W * p.n : nullptr;
             if (obs_t && !(kAblate & 8u)) {
@@ -2358,6 +2436,15 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 if ((WT || 4 * q < W) && 4 * q + lrow < W)
                     *reinterpret_cast<uint4 *>(&OV[(4 * q + lrow + kPad) * kWave + lcc]) = make_uint4(0u, 0u, 0u, 0u);
             if (lane == 0) lds_flag_set(&sm.fq, (uint32_t)t + 1u);  // the logic wave may change the planes
+            if constexpr (CHO) {
+                const int npg = mt_chunk_store<0>(orm, lane, ch);
+                if (ch.l >= 0) {
+                    last_l = ch.l;
+                    last_cur = ch.cur;
+                    last_pg = npg;
+                    if (lane == last_l) sm.cpg[lane] = 0x80000000u | ((uint32_t)last_cur << 10) | (uint32_t)last_pg;
+                }
+            }
             stamp(2);
         }
         wg_barrier();
