@@ -19,5 +19,5 @@ for n in 65536 32768; do
       AB_N=$n ST_LIB=$lib AB_LABEL="$(basename $lib) n=$n" timeout -k 10 120 python tools/ab_rollout.py 100 10 f32 || exit 1
     done
   done
-done | tee gpurun_out/ab_$TAG.txt
+done | tee gpurun_out/ab_vs_base_$TAG.txt
 timeout -k 10 120 python tools/ro_stamps.py 100 6 | tee gpurun_out/stamps_$TAG.txt
