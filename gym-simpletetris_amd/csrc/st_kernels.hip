@@ -2351,102 +2351,126 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
         // racing it writes the same values).
         [[maybe_unused]] const MtRes orm = mt_res(p.mt + e0 * kMtPitch, lane);
         [[maybe_unused]] int last_l = -1, last_cur = 0, last_pg = 0;
-        for (int t = 0; t < K; ++t) {
-            lds_flag_wait_ge(&sm.fo, (uint32_t)t + 1u);
-            // the chunk's operands, issued before the obs stores (their
-            // latency overlaps them, and the wait for them does not wait for
-            // the stores: one in-order vmcnt)
-            [[maybe_unused]] MtChunk ch;
-            if constexpr (CHO) {
-                const uint32_t w = sm.cw[lane];
-                int pg = (int)(w & 0x3FFu);
-                const int cur = (int)((w >> 10) & 1u);
-                if (lane == last_l && cur == last_cur && last_pg > pg) pg = last_pg;
-                mt_chunk_issue_pc(orm, (w >> 31) != 0u && pg < kMtN, pg, cur, lane, ch);
+        // a chunk's operands are issued at the end of a step and its words
+        // computed and stored after the next step's obs stores: the loads have
+        // a whole step to arrive, and the obs of a step never waits for them
+        // (one in-order vmcnt: the wait covers only what was issued before)
+        [[maybe_unused]] MtChunk ch;
+        ch.l = -1;
+        auto chunk_next = [&]() {
+            const uint32_t w = sm.cw[lane];
+            int pg = (int)(w & 0x3FFu);
+            const int cur = (int)((w >> 10) & 1u);
+            if (lane == last_l && cur == last_cur && last_pg > pg) pg = last_pg;
+            mt_chunk_issue_pc(orm, (w >> 31) != 0u && pg < kMtN, pg, cur, lane, ch);
+        };
+        auto chunk_done = [&]() {
+            const int npg = mt_chunk_store<0>(orm, lane, ch);
+            if (ch.l >= 0) {
+                last_l = ch.l;
+                last_cur = ch.cur;
+                last_pg = npg;
+                if (lane == last_l) sm.cpg[lane] = 0x80000000u | ((uint32_t)last_cur << 10) | (uint32_t)last_pg;
             }
-            stamp(1);
-            uint32_t *const obs_t = p.obs ? p.obs + (int64_t)t * W * p.n : nullptr;
-            if (obs_t && !(kAblate & 8u)) {
-                if (wide_obs) {
-                    const auto ro = buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u);
-                    const uint32_t noff = (uint32_t)lrow * (uint32_t)p.n + (uint32_t)lcc;
-#pragma unroll
-                    for (int q = 0; q < NBQ; ++q) {
-                        if ((WT || 4 * q < W) && 4 * q + lrow < W) {
-                            const int i = (4 * q + lrow + kPad) * kWave + lcc;
-                            uint4 v = *reinterpret_cast<const uint4 *>(&L[i]);
-                            const uint4 o = *reinterpret_cast<const uint4 *>(&OV[i]);
-                            v.x = (v.x | o.x) & hmask;
-                            v.y = (v.y | o.y) & hmask;
-                            v.z = (v.z | o.z) & hmask;
-                            v.w = (v.w | o.w) & hmask;
-                            buf_store16<kNT>(ro, ((uint32_t)e0 + (uint32_t)(4 * q) * (uint32_t)p.n + noff) * 4u, v);
+        };
+        // one loop per obs mode (wave-uniform for the launch): the mode fixes
+        // the number of obs stores per step, so the compiler's vmcnt for the
+        // previous step's chunk operands counts exactly (with a runtime
+        // branch it took the smallest count over the paths and waited for
+        // the obs stores too)
+        auto out_loop = [&](auto om_c) {
+            constexpr int OM = decltype(om_c)::value;  // 0: no packed obs, 1: 16-B rows, 2: one dword per row
+            for (int t = 0; t < K; ++t) {
+                lds_flag_wait_ge(&sm.fo, (uint32_t)t + 1u);
+                stamp(1);
+                uint32_t *const obs_t = p.obs ? p.obs + (int64_t)t * W * p.n : nullptr;
+                if constexpr (OM != 0) {
+                    if constexpr (OM == 1) {
+                        const auto ro = buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u);
+                        const uint32_t noff = (uint32_t)lrow * (uint32_t)p.n + (uint32_t)lcc;
+    #pragma unroll
+                        for (int q = 0; q < NBQ; ++q) {
+                            if (WT || 4 * q < W) {
+                                // rows past W (the last group's spare lanes) read
+                                // the wall columns and store with an out-of-range
+                                // offset: no branch around the store, so every
+                                // step issues the same stores (exact vmcnt counts)
+                                const bool on = 4 * q + lrow < W;
+                                const int i = (4 * q + lrow + kPad) * kWave + lcc;
+                                uint4 v = *reinterpret_cast<const uint4 *>(&L[i]);
+                                const uint4 o = *reinterpret_cast<const uint4 *>(&OV[i]);
+                                v.x = (v.x | o.x) & hmask;
+                                v.y = (v.y | o.y) & hmask;
+                                v.z = (v.z | o.z) & hmask;
+                                v.w = (v.w | o.w) & hmask;
+                                buf_store16<kNT>(
+                                    ro, on ? ((uint32_t)e0 + (uint32_t)(4 * q) * (uint32_t)p.n + noff) * 4u : kOff, v);
+                            }
+                        }
+                    } else if (real) {  // ragged / unaligned: one dword per row (rare: not tuned)
+                        const auto ro = buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u);
+    #pragma unroll 1
+                        for (int x = 0; x < W; ++x)
+                            __builtin_amdgcn_raw_buffer_store_b32((col(L, x) | col(OV, x)) & hmask, ro,
+                                                                  ((uint32_t)x * (uint32_t)p.n + (uint32_t)e) * 4u, 0, kNT);
+                    }
+                }
+                if constexpr (F32) {
+                    // float32 obs [n][W][H] of the wave's envs: one contiguous block,
+                    // lane-consecutive float4 chunks, non-temporal (A/B: -13% f32 rollout)
+                    const int64_t nreal64 = p.n - e0 < kWave ? p.n - e0 : kWave;
+                    const int nreal = (int)nreal64;
+                    float *out = p.obs_f32 + ((int64_t)t * p.n + e0) * (W * H);
+                    if constexpr (WT != 0 && HT % 4 == 0) {
+                        constexpr int CPC = HT / 4, CPE = WT * CPC;
+                        uint32_t *O = sm.O;
+    #pragma unroll
+                        for (int x = 0; x < WT; ++x) O[lane * (WT + 1) + x] = (col(L, x) | col(OV, x)) & hmask;
+                        wave_sync();
+                        float4 *out4 = reinterpret_cast<float4 *>(out);
+                        const float4 *F4 = reinterpret_cast<const float4 *>(sm.F4);
+                        const int total = nreal * CPE;
+                        for (int c = lane; c < total; c += kWave) {
+                            const int ee = c / CPE;
+                            const int cr = c - ee * CPE;
+                            const int x = cr / CPC;
+                            const int q = cr - x * CPC;
+                            const float4 f = F4[(O[ee * (WT + 1) + x] >> (4 * q)) & 15u];
+                            typedef float f32x4 __attribute__((ext_vector_type(4)));
+                            const f32x4 fv = {f.x, f.y, f.z, f.w};
+                            __builtin_nontemporal_store(fv, reinterpret_cast<f32x4 *>(&out4[c]));
+                        }
+                        wave_sync();  // staging reads done before the next step's writes
+                    } else {
+                        const int per_env = W * H;
+                        const int total = nreal * per_env;
+                        for (int f = lane; f < total; f += kWave) {
+                            const int ee = f / per_env;
+                            const int rem = f - ee * per_env;
+                            const int x = rem / H;
+                            const int y = rem - x * H;
+                            const uint32_t w = (L[(x + kPad) * kWave + ee] | OV[(x + kPad) * kWave + ee]) & hmask;
+                            out[f] = (float)((w >> y) & 1u);
                         }
                     }
-                } else if (real) {  // ragged / unaligned: one dword per row
-                    const auto ro = buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u);
-#pragma unroll 1
-                    for (int x = 0; x < W; ++x)
-                        __builtin_amdgcn_raw_buffer_store_b32((col(L, x) | col(OV, x)) & hmask, ro,
-                                                              ((uint32_t)x * (uint32_t)p.n + (uint32_t)e) * 4u, 0, kNT);
                 }
-            }
-            if constexpr (F32) {
-                // float32 obs [n][W][H] of the wave's envs: one contiguous block,
-                // lane-consecutive float4 chunks, non-temporal (A/B: -13% f32 rollout)
-                const int64_t nreal64 = p.n - e0 < kWave ? p.n - e0 : kWave;
-                const int nreal = (int)nreal64;
-                float *out = p.obs_f32 + ((int64_t)t * p.n + e0) * (W * H);
-                if constexpr (WT != 0 && HT % 4 == 0) {
-                    constexpr int CPC = HT / 4, CPE = WT * CPC;
-                    uint32_t *O = sm.O;
-#pragma unroll
-                    for (int x = 0; x < WT; ++x) O[lane * (WT + 1) + x] = (col(L, x) | col(OV, x)) & hmask;
-                    wave_sync();
-                    float4 *out4 = reinterpret_cast<float4 *>(out);
-                    const float4 *F4 = reinterpret_cast<const float4 *>(sm.F4);
-                    const int total = nreal * CPE;
-                    for (int c = lane; c < total; c += kWave) {
-                        const int ee = c / CPE;
-                        const int cr = c - ee * CPE;
-                        const int x = cr / CPC;
-                        const int q = cr - x * CPC;
-                        const float4 f = F4[(O[ee * (WT + 1) + x] >> (4 * q)) & 15u];
-                        typedef float f32x4 __attribute__((ext_vector_type(4)));
-                        const f32x4 fv = {f.x, f.y, f.z, f.w};
-                        __builtin_nontemporal_store(fv, reinterpret_cast<f32x4 *>(&out4[c]));
-                    }
-                    wave_sync();  // staging reads done before the next step's writes
-                } else {
-                    const int per_env = W * H;
-                    const int total = nreal * per_env;
-                    for (int f = lane; f < total; f += kWave) {
-                        const int ee = f / per_env;
-                        const int rem = f - ee * per_env;
-                        const int x = rem / H;
-                        const int y = rem - x * H;
-                        const uint32_t w = (L[(x + kPad) * kWave + ee] | OV[(x + kPad) * kWave + ee]) & hmask;
-                        out[f] = (float)((w >> y) & 1u);
-                    }
+                wave_sync();  // every read of the overlay plane precedes its clearing
+    #pragma unroll
+                for (int q = 0; q < NBQ; ++q)
+                    if ((WT || 4 * q < W) && 4 * q + lrow < W)
+                        *reinterpret_cast<uint4 *>(&OV[(4 * q + lrow + kPad) * kWave + lcc]) = make_uint4(0u, 0u, 0u, 0u);
+                if (lane == 0) lds_flag_set(&sm.fq, (uint32_t)t + 1u);  // the logic wave may change the planes
+                if constexpr (CHO) {
+                    chunk_done();  // the previous step's (none at t = 0: ch.l < 0)
+                    chunk_next();
                 }
+                stamp(2);
             }
-            wave_sync();  // every read of the overlay plane precedes its clearing
-#pragma unroll
-            for (int q = 0; q < NBQ; ++q)
-                if ((WT || 4 * q < W) && 4 * q + lrow < W)
-                    *reinterpret_cast<uint4 *>(&OV[(4 * q + lrow + kPad) * kWave + lcc]) = make_uint4(0u, 0u, 0u, 0u);
-            if (lane == 0) lds_flag_set(&sm.fq, (uint32_t)t + 1u);  // the logic wave may change the planes
-            if constexpr (CHO) {
-                const int npg = mt_chunk_store<0>(orm, lane, ch);
-                if (ch.l >= 0) {
-                    last_l = ch.l;
-                    last_cur = ch.cur;
-                    last_pg = npg;
-                    if (lane == last_l) sm.cpg[lane] = 0x80000000u | ((uint32_t)last_cur << 10) | (uint32_t)last_pg;
-                }
-            }
-            stamp(2);
-        }
+        };
+        if (!p.obs || (kAblate & 8u)) out_loop(std::integral_constant<int, 0>{});
+        else if (wide_obs) out_loop(std::integral_constant<int, 1>{});
+        else out_loop(std::integral_constant<int, 2>{});
+        if constexpr (CHO) chunk_done();
         wg_barrier();
     }
     // ---- counter rows this wave owns (logic: 0-5 and the piece row, draw:
