@@ -1744,6 +1744,8 @@ struct RoLds {
     uint32_t qring[kWave];  // per lane: the env's i-th queued piece in bits 4 (i & 3) .. (draw -> logic)
     uint32_t cm[2][2];      // step t's consumption mask (a spawn or a same-step reset) in cm[t & 1]
     uint32_t act[4][kWave];  // step t's actions in act[t & 3] (draw -> logic, four steps ahead)
+    uint32_t rw[2][kWave], dn[2][kWave];  // step t's reward / done in [t & 1] (logic -> output)
+    uint32_t ep[2][4][kWave];             // a same-step reset's episode time / score / lines / holes
     // packed obs (the output wave builds the next-generation chunks):
     uint32_t cw[kWave];   // per lane: chunk candidate << 31 | cur << 10 | pg (draw -> output)
     uint32_t cpg[kWave];  // per lane: valid << 31 | cur << 10 | pg after a chunk (output -> draw)
@@ -1962,12 +1964,12 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             // two initial draws count as one round) and its descriptors, for a
             // spawn below (read under the lock path); then the output wave's
             // reads of step t - 1's planes, before this step changes them
-            if (!(kAblate & 32u)) lds_flag_wait_ge(&sm.fd, t > 1 ? (uint32_t)t : 1u);
+            if (!(kAblate & 160u)) lds_flag_wait_ge(&sm.fd, t > 1 ? (uint32_t)t : 1u);
             const int sid = (int)((sm.qring[lane] >> (4u * (nq & 3u))) & 7u);
             uint2 s4[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) s4[r] = tab(sid * 4 + r);
-            if (!(kAblate & 32u)) lds_flag_wait_ge(&sm.fq, (uint32_t)t);
+            if (!(kAblate & 288u)) lds_flag_wait_ge(&sm.fq, (uint32_t)t);
             stamp(3);
 
             // ---- lock path (tetris_env.py:263-299) ----
@@ -2084,12 +2086,11 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 }
             }
             nq += draw ? 1u : 0u;
-            {
-                const auto rr = buf_rsrc(p.reward ? p.reward + (int64_t)t * p.n : nullptr, (uint32_t)p.n * 4u);
-                const auto rd = buf_rsrc(p.done ? p.done + (int64_t)t * p.n : nullptr, (uint32_t)p.n);
-                __builtin_amdgcn_raw_buffer_store_b32(rew, rr, real ? (uint32_t)e * 4u : kOff, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b8((char)(died ? 1 : 0), rd, real ? (uint32_t)e : kOff, 0, 0);
-            }
+            // reward / done (and below a reset's episode counters) go to the
+            // output wave through LDS (step parity t & 1; it stores them with
+            // the obs): memory stores cost this chain ~2.5%, LDS writes less
+            sm.rw[t & 1][lane] = (uint32_t)rew;
+            sm.dn[t & 1][lane] = died ? 1u : 0u;
             stamp(5);
             // ---- this step's obs (tetris_env.py:301-302) for the output wave ----
             // a death without auto-reset: the board loses the piece (R8,
@@ -2116,23 +2117,14 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                     }
                 }
             }
-            {
-                // the finished episode's counters (ST_AUTORESET_SAME_STEP):
-                // unconditional buffer stores, dropped (out-of-range offset)
-                // for lanes that did not reset -- a store under a branch would
-                // leave the compiler's vmcnt count unknown at the next step's
-                // action-load wait, which then waited for this step's stores
-                const auto rs = buf_rsrc(p.stats, (uint32_t)ST_NSTAT * (uint32_t)sd * 4u);
-                const uint32_t eo = (uint32_t)e * 4u;
-                auto put = [&](int row, int32_t v) {
-                    __builtin_amdgcn_raw_buffer_store_b32(v, rs, reset_now ? eo + (uint32_t)row * (uint32_t)sd * 4u : kOff,
-                                                          0, 0);
-                };
-                put(ST_STAT_EP_TIME, time);
-                put(ST_STAT_EP_SCORE, score);
-                put(ST_STAT_EP_LINES, lines);
-                put(ST_STAT_EP_HOLES, holes);
-                if (reset_now) time = score = lines = holes = height = 0;
+            if (reset_now) {
+                // the finished episode's counters (ST_AUTORESET_SAME_STEP),
+                // stored by the output wave where done is set
+                sm.ep[t & 1][0][lane] = (uint32_t)time;
+                sm.ep[t & 1][1][lane] = (uint32_t)score;
+                sm.ep[t & 1][2][lane] = (uint32_t)lines;
+                sm.ep[t & 1][3][lane] = (uint32_t)holes;
+                time = score = lines = holes = height = 0;
             }
             if (lane == 0) lds_flag_set(&sm.fo, (uint32_t)t + 1u);
             // ---- state for the next step ----
@@ -2459,6 +2451,25 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 for (int q = 0; q < NBQ; ++q)
                     if ((WT || 4 * q < W) && 4 * q + lrow < W)
                         *reinterpret_cast<uint4 *>(&OV[(4 * q + lrow + kPad) * kWave + lcc]) = make_uint4(0u, 0u, 0u, 0u);
+                {
+                    // reward / done of step t (and a reset's episode counters): branch-free
+                    // stores, out-of-range offsets where there is nothing to store
+                    const auto rr = buf_rsrc(p.reward ? p.reward + (int64_t)t * p.n : nullptr, (uint32_t)p.n * 4u);
+                    const auto rd = buf_rsrc(p.done ? p.done + (int64_t)t * p.n : nullptr, (uint32_t)p.n);
+                    const uint32_t dn = sm.dn[t & 1][lane];
+                    if (!(kAblate & 64u)) {
+                        __builtin_amdgcn_raw_buffer_store_b32(sm.rw[t & 1][lane], rr, real ? (uint32_t)e * 4u : kOff, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b8((char)dn, rd, real ? (uint32_t)e : kOff, 0, 0);
+                        const bool rs_now = dn != 0u && p.autoreset == ST_AUTORESET_SAME_STEP;
+                        const auto rs = buf_rsrc(p.stats, (uint32_t)ST_NSTAT * (uint32_t)sd * 4u);
+                        const uint32_t eo = (uint32_t)e * 4u;
+                        constexpr int kEpRow[4] = {ST_STAT_EP_TIME, ST_STAT_EP_SCORE, ST_STAT_EP_LINES, ST_STAT_EP_HOLES};
+#pragma unroll
+                        for (int k = 0; k < 4; ++k)
+                            __builtin_amdgcn_raw_buffer_store_b32(sm.ep[t & 1][k][lane], rs,
+                                                                  rs_now ? eo + (uint32_t)kEpRow[k] * (uint32_t)sd * 4u : kOff, 0, 0);
+                    }
+                }
                 if (lane == 0) lds_flag_set(&sm.fq, (uint32_t)t + 1u);  // the logic wave may change the planes
                 if constexpr (CHO) {
                     chunk_done();  // the previous step's (none at t = 0: ch.l < 0)

@@ -2,13 +2,13 @@
 # Timing-only ablations of the queued-draw st_rollout (results are NOT valid
 # games), 65,536 envs, 100-step launches: 0 = none, 1 = no lock path, 2 = no
 # draws, 8 = no obs output, 16 = no next-generation chunk, 32 = the logic
-# wave never waits for the draw / output waves.
+# wave never waits for the draw / output waves, 64 = no reward / done / episode-counter stores in the logic wave, 128 = the logic wave never waits for the draw wave (fd), 256 = never for the output wave (fq).
 # Needs: make -C gym-simpletetris_amd/csrc variant V=ablation DEFS=-DST_ABLATION=1
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"; mkdir -p gpurun_out
 A=$R/gym-simpletetris_amd/csrc/build/lib_ablation.so
 TAG=${TAG:-roq}
-for ab in 0 1 2 16 32 34 0; do
+for ab in 0 32 64 128 256 0; do
   AB_LABEL="ablate=$ab" ST_LIB=$A ST_ABLATE=$ab timeout -k 10 120 python tools/ab_rollout.py 100 10 || exit 1
 done | tee gpurun_out/roq_ablate_$TAG.txt
 cd /tmp && export TMPDIR=/tmp
