@@ -5,5 +5,5 @@ set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"
 for i in 1 2 3 4 5 6 7 8; do
   timeout -k 10 120 python bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline 2>/dev/null \
-   | python -c "import json,sys; d=json.load(sys.stdin); print(json.dumps({'run': $i, 'value': d['value'], 'ms_per_step': d['ms_per_step'], 'kernel_us': d['roofline']['kernel_us']}))" || exit 1
+   | python -c "import json,sys; d=json.load(sys.stdin); print(json.dumps({'run': $i, 'value': d['value'], 'ms_per_step': d['ms_per_step'], 'event_us_per_launch': d['roofline']['event_us_per_launch'], 'steady_us': d['roofline']['steady']['event_us_per_launch']}))" || exit 1
 done
