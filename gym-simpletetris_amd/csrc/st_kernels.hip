@@ -2206,6 +2206,9 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             q1 = draw_win<CHO>(real, cq, mta, win, o, wlim, mtg, sm.S, lane);
             c1 = mt_consumed(m0, mta);
         }
+        int32_t cq[7];  // shape counts once the queue's head has spawned
+#pragma unroll
+        for (int i = 0; i < 7; ++i) cq[i] = cnt_r[i] + (i == q0);
         uint32_t qw = (uint32_t)q0 | ((uint32_t)q1 << 4), nd = 2;  // the ring word, pieces drawn
         sm.qring[lane] = qw;
         sm.act[0][lane] = a0;
@@ -2250,15 +2253,16 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             }
             // step s consumed q0: count it (_new_piece :199), commit q1 as the
             // preview, draw the piece after it
+            // (cq = cnt_r + the head's count is kept across rounds: a spawn
+            // makes cnt_r = cq, and the new head q1 adds its own)
 #pragma unroll
-            for (int i = 0; i < 7; ++i) cnt_r[i] += (cons && i == q0);
+            for (int i = 0; i < 7; ++i) cnt_r[i] = cons ? cq[i] : cnt_r[i];
             if (cons) {
                 mtc = pv_pack(mta, q1, c1);
                 q0 = q1;
             }
-            int32_t cq[7];
 #pragma unroll
-            for (int i = 0; i < 7; ++i) cq[i] = cnt_r[i] + (i == q0);
+            for (int i = 0; i < 7; ++i) cq[i] += (cons && i == q0);
             const uint32_t m0 = mta;
             const int pk = draw_win<CHO>(cons, cq, mta, win, o, wlim, mtg, sm.S, lane);
             if (cons) {
@@ -2372,12 +2376,43 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
         // the obs stores too)
         auto out_loop = [&](auto om_c) {
             constexpr int OM = decltype(om_c)::value;  // 0: no packed obs, 1: 16-B rows, 2: one dword per row
+            // (WT: the 16-B row groups read once per lane, compile-time rows)
+            constexpr bool EARLY = OM == 1 && !F32 && WT != 0;
             for (int t = 0; t < K; ++t) {
                 lds_flag_wait_ge(&sm.fo, (uint32_t)t + 1u);
                 stamp(1);
                 uint32_t *const obs_t = p.obs ? p.obs + (int64_t)t * W * p.n : nullptr;
                 if constexpr (OM != 0) {
-                    if constexpr (OM == 1) {
+                    if constexpr (EARLY) {
+                        // read the planes, clear the overlay, raise fq, THEN
+                        // store: the logic wave waits for fq before it changes
+                        // a plane, and only the reads have to precede that
+                        // (timing ablation: that wait cost the logic ~2%)
+                        const auto ro = buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u);
+                        const uint32_t noff = (uint32_t)lrow * (uint32_t)p.n + (uint32_t)lcc;
+                        uint4 ob[NBQ];
+    #pragma unroll
+                        for (int q = 0; q < NBQ; ++q) {
+                            const int i = (4 * q + lrow + kPad) * kWave + lcc;
+                            const uint4 v = *reinterpret_cast<const uint4 *>(&L[i]);
+                            const uint4 o = *reinterpret_cast<const uint4 *>(&OV[i]);
+                            ob[q] = make_uint4((v.x | o.x) & hmask, (v.y | o.y) & hmask, (v.z | o.z) & hmask,
+                                               (v.w | o.w) & hmask);
+                        }
+    #pragma unroll
+                        for (int q = 0; q < NBQ; ++q)  // (each lane clears the slots it read)
+                            if (4 * q + lrow < W)
+                                *reinterpret_cast<uint4 *>(&OV[(4 * q + lrow + kPad) * kWave + lcc]) =
+                                    make_uint4(0u, 0u, 0u, 0u);
+                        if (lane == 0) lds_flag_set(&sm.fq, (uint32_t)t + 1u);  // the logic wave may change the planes
+    #pragma unroll
+                        for (int q = 0; q < NBQ; ++q)
+                            buf_store16<kNT>(ro,
+                                             4 * q + lrow < W
+                                                 ? ((uint32_t)e0 + (uint32_t)(4 * q) * (uint32_t)p.n + noff) * 4u
+                                                 : kOff,
+                                             ob[q]);
+                    } else if constexpr (OM == 1) {
                         const auto ro = buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u);
                         const uint32_t noff = (uint32_t)lrow * (uint32_t)p.n + (uint32_t)lcc;
     #pragma unroll
@@ -2446,11 +2481,14 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                         }
                     }
                 }
-                wave_sync();  // every read of the overlay plane precedes its clearing
+                if constexpr (!EARLY) {
+                    wave_sync();  // every read of the overlay plane precedes its clearing
     #pragma unroll
-                for (int q = 0; q < NBQ; ++q)
-                    if ((WT || 4 * q < W) && 4 * q + lrow < W)
-                        *reinterpret_cast<uint4 *>(&OV[(4 * q + lrow + kPad) * kWave + lcc]) = make_uint4(0u, 0u, 0u, 0u);
+                    for (int q = 0; q < NBQ; ++q)
+                        if ((WT || 4 * q < W) && 4 * q + lrow < W)
+                            *reinterpret_cast<uint4 *>(&OV[(4 * q + lrow + kPad) * kWave + lcc]) =
+                                make_uint4(0u, 0u, 0u, 0u);
+                }
                 {
                     // reward / done of step t (and a reset's episode counters): branch-free
                     // stores, out-of-range offsets where there is nothing to store
@@ -2470,7 +2508,8 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                                                                   rs_now ? eo + (uint32_t)kEpRow[k] * (uint32_t)sd * 4u : kOff, 0, 0);
                     }
                 }
-                if (lane == 0) lds_flag_set(&sm.fq, (uint32_t)t + 1u);  // the logic wave may change the planes
+                if constexpr (!EARLY)
+                    if (lane == 0) lds_flag_set(&sm.fq, (uint32_t)t + 1u);  // the logic wave may change the planes
                 if constexpr (CHO) {
                     chunk_done();  // the previous step's (none at t = 0: ch.l < 0)
                     chunk_next();

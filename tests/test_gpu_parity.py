@@ -668,6 +668,41 @@ def test_rollout_equals_steps(autoreset, board):
             assert np.array_equal(sa[k], sb[k]), (obs_mode, k)
 
 
+@pytest.mark.parametrize("autoreset", ["same_step", "none"])
+def test_rollout_short_launches_queue_edges(autoreset):
+    """The three-wave st_rollout's piece queue and action ring at their edges:
+    launches of 1, 2, 3 and 5 steps (the action ring's first four rows come
+    from the draw wave's initial loads; the logic wave's first waits have
+    their own thresholds), hard drops on half the steps (a lock at most
+    steps: the queue drained two pieces deep while the draw wave lags), and
+    a state read-back in the middle (st_mt_sync: every env restarts without
+    a preview, so the first rollout after it draws q0 and q1 at its start).
+    Outputs and final state == the same steps through st_step."""
+    G = _engine()
+    n = 1000
+    kw = dict(width=10, height=20, advanced_clears=True, penalise_holes_increase=True)
+    a = G.TetrisBatch(n, autoreset=autoreset, seeds=[40 + e for e in range(n)], **kw)
+    b = G.TetrisBatch(n, autoreset=autoreset, seeds=[40 + e for e in range(n)], **kw)
+    a.reset()
+    b.reset()
+    lengths = [1, 2, 3, 5, 1, 1, 4, 3, 2, 5, 1]
+    T = 2 * sum(lengths)
+    acts = torch.stack([a.gen_actions(t, 23).clone() for t in range(T)])
+    acts[::2] = 2  # hard drops
+    t = 0
+    for rep in range(2):
+        for k in lengths:
+            ro, rr, rd = a.rollout(acts[t:t + k], obs="packed")
+            for j in range(k):
+                so, sr, sd = b.step(acts[t + j], obs="packed")
+                assert torch.equal(so, ro[j]), (rep, t, j)
+                assert torch.equal(sr, rr[j]) and torch.equal(sd, rd[j]), (rep, t, j)
+            t += k
+        sa, sb = a.get_state(), b.get_state()  # synced: no preview in either afterwards
+        for key in sa:
+            assert np.array_equal(sa[key], sb[key]), (rep, key)
+
+
 def test_rollout_vs_oracle_full_size():
     """N = 65,536, K = 32 steps in one launch vs the C oracle."""
     G = _engine()
