@@ -1905,15 +1905,17 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
         for (int r = 0; r < 4; ++r) d4[r] = tab((int)(pw & 7u) * 4 + r);
         bool bad_act = false;
         uint32_t nq = 0;  // pieces this env consumed so far (its next spawn: ring slot nq & 3)
+        // The actions come from the ring the draw wave fills four steps ahead
+        // (at the end of round t - 4, or its initial loads for t < 4, published
+        // by round t - 3's fd): LDS reads, no memory wait on this chain (CDNA
+        // counts loads and stores in one in-order vmcnt: a load here waited
+        // for the previous step's stores as well).  Step t + 1's is read in
+        // step t right after the queue wait (fd >= t covers it), so a step
+        // starts with its action in a register: no poll, no LDS round trip.
+        lds_flag_wait_ge(&sm.fd, 1u);
+        uint32_t act_n = sm.act[0][lane];
         for (int t = 0; t < K; ++t) {
-            // the action, from the ring the draw wave fills four steps ahead
-            // (at the end of round t - 4, or its initial loads for t < 4),
-            // published by round t - 3's fd: an LDS read, no
-            // memory wait on this chain (CDNA counts loads and stores in one
-            // in-order vmcnt: a load here waited for the previous step's
-            // reward / done / counter stores as well)
-            lds_flag_wait_ge(&sm.fd, t > 2 ? (uint32_t)t - 1u : 1u);
-            const uint32_t act = real ? sm.act[t & 3][lane] : 6u;
+            const uint32_t act = real ? act_n : 6u;
             bad_act |= act > 6u;
             int rot = (int)((pw >> 3) & 3u);
             int ax = (int)((pw >> 5) & 63u);
@@ -1965,6 +1967,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             // spawn below (read under the lock path); then the output wave's
             // reads of step t - 1's planes, before this step changes them
             if (!(kAblate & 160u)) lds_flag_wait_ge(&sm.fd, t > 1 ? (uint32_t)t : 1u);
+            act_n = sm.act[(t + 1) & 3][lane];  // step t + 1's (a stale row past the last step: unused)
             const int sid = (int)((sm.qring[lane] >> (4u * (nq & 3u))) & 7u);
             uint2 s4[4];
 #pragma unroll
@@ -2232,14 +2235,12 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 return cc ^ (pv_ok(mtc) && ic <= (int)((mtc >> 25) & kPvCMax) ? 1 : 0);
             };
             [[maybe_unused]] MtChunk chunk;
+            // the output wave's finished chunks, read now and applied after
+            // the draw (the read's latency off this chain; a progress one
+            // round staler only means a rarer, same-valued mt_finish)
+            [[maybe_unused]] uint32_t cpgv = 0;
             if constexpr (CHO) {
-                // the output wave's finished chunks: the progress, where the
-                // generation is still the one the chunk was built for
-                const uint32_t v = sm.cpg[lane];
-                int ia, pga, ca;
-                mt_unpack(mta, ia, pga, ca);
-                if ((v >> 31) && (int)((v >> 10) & 1u) == ca && (int)(v & 0x3FFu) > pga)
-                    mta = mt_pack(ia, (int)(v & 0x3FFu), ca);
+                cpgv = sm.cpg[lane];
             } else {
                 mt_chunk_issue(mrs, mta, real && ref_cur() == (int)((mta >> 20) & 1u) && !(kAblate & 16u), lane,
                                chunk);
@@ -2277,11 +2278,17 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             stamp(3);
             [[maybe_unused]] int chunk_pg = 0;
             if constexpr (CHO) {
+                // the progress, where the generation is still the one the
+                // chunk was built for
+                int ia, pga, ca;
+                mt_unpack(mta, ia, pga, ca);
+                if ((cpgv >> 31) && (int)((cpgv >> 10) & 1u) == ca && (int)(cpgv & 0x3FFu) > pga) {
+                    pga = (int)(cpgv & 0x3FFu);
+                    mta = mt_pack(ia, pga, ca);
+                }
                 // this env's chunk candidacy for the output wave: the
                 // reference state in the generation mta is in, successor
                 // incomplete
-                int ia, pga, ca;
-                mt_unpack(mta, ia, pga, ca);
                 const bool cand = real && ref_cur() == ca && pga < kMtN && !(kAblate & 16u);
                 sm.cw[lane] = (cand ? 0x80000000u : 0u) | ((uint32_t)ca << 10) | (uint32_t)pga;
             } else {
