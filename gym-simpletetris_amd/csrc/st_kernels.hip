@@ -823,6 +823,10 @@ __device__ __forceinline__ void lds_flag_wait(uint32_t *f, uint32_t v) {
         __builtin_amdgcn_s_sleep(1);
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
+// A progress counter read as a relaxed LDS atomic (no wait by itself).
+__device__ __forceinline__ uint32_t lds_flag_get(uint32_t *f) {
+    return __hip_atomic_load((lds_u32 *)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 // The same for a progress counter that the writer may have advanced past v.
 __device__ __forceinline__ void lds_flag_wait_ge(uint32_t *f, uint32_t v) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -1966,13 +1970,29 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             // two initial draws count as one round) and its descriptors, for a
             // spawn below (read under the lock path); then the output wave's
             // reads of step t - 1's planes, before this step changes them
-            if (!(kAblate & 160u)) lds_flag_wait_ge(&sm.fd, t > 1 ? (uint32_t)t : 1u);
-            act_n = sm.act[(t + 1) & 3][lane];  // step t + 1's (a stale row past the last step: unused)
-            const int sid = (int)((sm.qring[lane] >> (4u * (nq & 3u))) & 7u);
+            // both counters and the ring words they guard in one LDS round
+            // trip (the writers store the data before the counters; see the
+            // draw wave's mask wait): step t + 1's action (a stale row past
+            // the last step: unused) and the queue word
+            uint32_t qwd;
+            {
+                const uint32_t need_d = t > 1 ? (uint32_t)t : 1u;
+                for (;;) {
+                    const uint32_t fdv = lds_flag_get(&sm.fd), fqv = lds_flag_get(&sm.fq);
+                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                    act_n = sm.act[(t + 1) & 3][lane];
+                    qwd = sm.qring[lane];
+                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                    const bool ok_d = (kAblate & 160u) || (int32_t)(fdv - need_d) >= 0;
+                    const bool ok_q = (kAblate & 288u) || (int32_t)(fqv - (uint32_t)t) >= 0;
+                    if (ok_d && ok_q) break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            const int sid = (int)((qwd >> (4u * (nq & 3u))) & 7u);
             uint2 s4[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) s4[r] = tab(sid * 4 + r);
-            if (!(kAblate & 288u)) lds_flag_wait_ge(&sm.fq, (uint32_t)t);
             stamp(3);
 
             // ---- lock path (tetris_env.py:263-299) ----
@@ -2245,13 +2265,22 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 mt_chunk_issue(mrs, mta, real && ref_cur() == (int)((mta >> 20) & 1u) && !(kAblate & 16u), lane,
                                chunk);
             }
-            lds_flag_wait_ge(&sm.fl, (uint32_t)s + 1u);
-            stamp(2);
-            bool cons;
-            {
-                const uint32_t w = lane < 32 ? sm.cm[s & 1][0] : sm.cm[s & 1][1];
-                cons = real && ((w >> (lane & 31)) & 1u) && !(kAblate & 2u);
+            // the counter and the mask it guards in one LDS round trip: a
+            // wave's LDS accesses execute in order and the logic wave writes
+            // the mask before the counter, so a mask read issued right after
+            // a counter read that passes is current (only the compiler must
+            // not reorder them: a signal fence, no wait)
+            uint32_t w;
+            for (;;) {
+                const uint32_t f = lds_flag_get(&sm.fl);
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                w = lane < 32 ? sm.cm[s & 1][0] : sm.cm[s & 1][1];
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                if ((int32_t)(f - ((uint32_t)s + 1u)) >= 0) break;
+                __builtin_amdgcn_s_sleep(1);
             }
+            stamp(2);
+            const bool cons = real && ((w >> (lane & 31)) & 1u) && !(kAblate & 2u);
             // step s consumed q0: count it (_new_piece :199), commit q1 as the
             // preview, draw the piece after it
             // (cq = cnt_r + the head's count is kept across rounds: a spawn
