@@ -1418,16 +1418,32 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             mt_unpack(mt_out, i2, pg2, c2);
             mt_out = mt_keep(mt_out, mt_pack(i2, chunk_pg, c2));
         }
-        if (dr || chunk_me) {
-            ss(ST_STAT_MT_INDEX) = mt_out;
-            sdd = 1u << ST_STAT_MT_INDEX;
-        }
-        if (dr) {
-            atomicAdd(&ss(ST_STAT_COUNT0 + sid), 1u);  // shape_counts[name] += 1, :199 (ds_add, no return)
-            sdd |= 1u << (ST_STAT_COUNT0 + sid);
+        if constexpr (STEP2) {
+            // st_step: this wave's changed counter rows straight from the
+            // registers, one coalesced dword per lane and row (no staging
+            // through LDS at the end of the chain): the MT word, and the
+            // count of the spawned shape (cnt[sid], already counted above)
+            int32_t csid = cnt[0];
+#pragma unroll
+            for (int i = 1; i < 7; ++i) csid = sid == i ? cnt[i] : csid;
+            const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
+            const uint32_t eo = (uint32_t)e * 4u;
+            __builtin_amdgcn_raw_buffer_store_b32(
+                mt_out, rs, dr || chunk_me ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff, 0, kNT);
+            __builtin_amdgcn_raw_buffer_store_b32(
+                (uint32_t)csid, rs, dr ? eo + (uint32_t)(ST_STAT_COUNT0 + sid) * (uint32_t)sd * 4u : kOff, 0, kNT);
+        } else {
+            if (dr || chunk_me) {
+                ss(ST_STAT_MT_INDEX) = mt_out;
+                sdd = 1u << ST_STAT_MT_INDEX;
+            }
+            if (dr) {
+                atomicAdd(&ss(ST_STAT_COUNT0 + sid), 1u);  // shape_counts[name] += 1, :199 (ds_add, no return)
+                sdd |= 1u << (ST_STAT_COUNT0 + sid);
+            }
         }
         if constexpr (KSTEPS == 1) {
-            if constexpr (TWO) sm.SDD[lane] = sdd;
+            if constexpr (STEP2) (void)sdd;  // (stored above)
             else sm.SD[lane] = sdd;  // the logic part ORs its rows in below
         } else if constexpr (TWO) {
             sm.mtw[t & 1][lane] = mt_out;  // the logic wave's next step reads it after B1
@@ -1468,23 +1484,40 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         }
         // st_step stores only the counter rows that changed (sdirty, per env)
         [[maybe_unused]] uint32_t sdirty = (1u << ST_STAT_TIME) | (1u << kPieceRow);
-        ss(ST_STAT_TIME) = (uint32_t)time;
-        ss(kPieceRow) = pw_out;
-        if (locknow) {
-            auto put = [&](int r, int32_t v, int32_t old) {
-                if constexpr (KSTEPS == 1) sdirty |= (uint32_t)(old != v) << r;
-                ss(r) = (uint32_t)v;
+        if constexpr (STEP2) {
+            // st_step: straight from the registers, one coalesced dword per
+            // lane and changed row (no staging through LDS at the end of the
+            // chain), unconditional stores with an out-of-range offset
+            // where a row did not change
+            const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
+            const uint32_t eo = (uint32_t)e * 4u;
+            auto put = [&](int r, int32_t v, bool on) {
+                __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, on ? eo + (uint32_t)r * (uint32_t)sd * 4u : kOff,
+                                                      0, kNT);
             };
-            put(ST_STAT_SCORE, score, o_score);
-            put(ST_STAT_LINES, lines, o_lines);
-            put(ST_STAT_HOLES, holes, o_holes);
-            put(ST_STAT_PIECE_HEIGHT, height, o_height);
-            put(ST_STAT_DEATHS, deaths, o_deaths);
+            put(ST_STAT_TIME, time, true);
+            put(kPieceRow, (int32_t)pw_out, true);
+            put(ST_STAT_SCORE, score, locknow && score != o_score);
+            put(ST_STAT_LINES, lines, locknow && lines != o_lines);
+            put(ST_STAT_HOLES, holes, locknow && holes != o_holes);
+            put(ST_STAT_PIECE_HEIGHT, height, locknow && height != o_height);
+            put(ST_STAT_DEATHS, deaths, locknow && deaths != o_deaths);
+        } else {
+            ss(ST_STAT_TIME) = (uint32_t)time;
+            ss(kPieceRow) = pw_out;
+            if (locknow) {
+                auto put = [&](int r, int32_t v, int32_t old) {
+                    if constexpr (KSTEPS == 1) sdirty |= (uint32_t)(old != v) << r;
+                    ss(r) = (uint32_t)v;
+                };
+                put(ST_STAT_SCORE, score, o_score);
+                put(ST_STAT_LINES, lines, o_lines);
+                put(ST_STAT_HOLES, holes, o_holes);
+                put(ST_STAT_PIECE_HEIGHT, height, o_height);
+                put(ST_STAT_DEATHS, deaths, o_deaths);
+            }
         }
-        if constexpr (KSTEPS == 1) {
-            if constexpr (TWO) sm.SD[lane] = sdirty;
-            else sm.SD[lane] |= sdirty;
-        }
+        if constexpr (KSTEPS == 1 && !STEP2) sm.SD[lane] |= sdirty;
 
         // ---- observation (tetris_env.py:301-302): board + current piece ----
         if constexpr (!(KSTEPS == 1 && TWO)) {
@@ -1612,7 +1645,9 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     // two waves: each stores the rows it owns (logic: 0-5 and the piece row,
     // draw: the shape counts and the MT word)
     uint32_t sdl = ~0u;
-    if constexpr (KSTEPS == 1) {
+    if constexpr (STEP2) {
+        // (stored per lane above)
+    } else if constexpr (KSTEPS == 1) {
         const uint32_t *sdm = ROLE == kRoleD ? sm.SDD : sm.SD;
         const uint4 sd4 = *reinterpret_cast<const uint4 *>(&sdm[lcc]);
         sdl = (sd4.x | sd4.y | sd4.z | sd4.w) >> lrow;
@@ -1624,6 +1659,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     const uint32_t soff = (uint32_t)e0 * 4u + loff * 4u;
 #pragma unroll
     for (int q = 0; q < kHotQ; ++q) {
+        if constexpr (STEP2) break;
         // row 15 (ep_time) is never staged: it is stored per lane on a reset
         if (((kOwn >> (4 * q)) & 0xFu) == 0u) continue;
         const bool st = ((kOwn >> (4 * q + lrow)) & 1u) && ((sdl >> (4 * q)) & 1u);
