@@ -538,18 +538,44 @@ __device__ __forceinline__ void draw_slow(bool &pending, uint32_t &r, int &idx, 
 // for a preview, which is counted when it spawns).
 // pre_pg: the next generation's progress when `pre` was loaded (-1: now);
 // its words past index 623 are usable only if that generation was complete.
-template <int WIN, bool COUNT = true>
-__device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t &mtst,
-                                          uint32_t *mt_wave, uint32_t *S, int lane,
-                                          const MtPre &pre, bool have_pre, int pre_pg = -1) {
+// The count-dependent part of a draw (randint's range n = sum(m), its
+// getrandbits width kb, and the prefix sums th[i] = m_0 + .. + m_i), split
+// off so that st_step's draw wave computes it before the lock decision: the
+// counts a spawn's preview draw sees are known at the start of the step
+// (the counts then + the preview's own shape; clear() keeps shape_counts).
+struct DrawPar {
+    uint32_t n;
+    int kb;
+    int32_t th[6];
+};
+__device__ __forceinline__ DrawPar draw_par(const int32_t (&cnt)[7]) {
     int32_t maxc = cnt[0], sumc = cnt[0];
 #pragma unroll
     for (int i = 1; i < 7; ++i) {
         maxc = cnt[i] > maxc ? cnt[i] : maxc;
         sumc += cnt[i];
     }
-    const uint32_t n = (uint32_t)(35 + 7 * maxc - sumc);
-    const int kb = 32 - __builtin_clz(n);
+    DrawPar d;
+    d.n = (uint32_t)(35 + 7 * maxc - sumc);
+    d.kb = 32 - __builtin_clz(d.n);
+    int32_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        sum += 5 + maxc - cnt[i];
+        d.th[i] = sum;
+    }
+    return d;
+}
+// The draw itself, for the lanes with `need` (see draw_shape): the window's
+// words are tempered 4 at a time (acceptance >= 1/2, ~0.7 typically; a second
+// group of 4 only in waves where a lane rejected 4 in a row), and the shape is
+// the number of prefix sums <= r (the first i with r + 1 <= th[i], :186-191:
+// independent compares, no serial chain).
+template <int WIN>
+__device__ __forceinline__ int draw_core(bool need, const DrawPar &dp, uint32_t &mtst, uint32_t *mt_wave,
+                                         uint32_t *S, int lane, const MtPre &pre, bool have_pre, int pre_pg = -1) {
+    const uint32_t n = dp.n;
+    const int kb = dp.kb;
     int idx, pg, cur;
     mt_unpack(mtst, idx, pg, cur);
     bool pending = need;
@@ -581,9 +607,13 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
                 pos = p0 + NW < lim ? p0 + NW : lim;
             }
         };
+        using I4 = std::integral_constant<int, 4>;
         using I8 = std::integral_constant<int, 8>;
         const int b = idx;
-        if (pending) pass(pre.w, b, I8{});
+        if (pending) pass(pre.w, b, I4{});
+        if (__ballot(pending && pos == b + 4)) {
+            if (pending && pos == b + 4) pass(pre.w + 4, b + 4, I4{});
+        }
         // 8 rejections in a row (p <= 2^-8 per draw, a few lanes per step):
         // the next 8 words are already here, no dependent load
         if constexpr (WIN > 8) {
@@ -601,20 +631,19 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
     draw_slow(pending, r, idx, pg, cur, n, kb, mt_wave, S, lane);
     if (need) mtst = mt_keep(mtst, mt_pack(idx, pg, cur));
     if (!need) return 0;
-    int32_t rr = (int32_t)r + 1;
-    int pick = 6;
-    bool found = false;
+    int pick = 0;
 #pragma unroll
-    for (int i = 0; i < 7; ++i) {
-        rr -= 5 + maxc - cnt[i];
-        if (!found && rr <= 0) {
-            pick = i;
-            found = true;
-        }
-    }
+    for (int i = 0; i < 6; ++i) pick += dp.th[i] <= (int32_t)r ? 1 : 0;
+    return pick;
+}
+template <int WIN, bool COUNT = true>
+__device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t &mtst,
+                                          uint32_t *mt_wave, uint32_t *S, int lane,
+                                          const MtPre &pre, bool have_pre, int pre_pg = -1) {
+    const int pick = draw_core<WIN>(need, draw_par(cnt), mtst, mt_wave, S, lane, pre, have_pre, pre_pg);
     if constexpr (COUNT) {
 #pragma unroll
-        for (int i = 0; i < 7; ++i) cnt[i] += (i == pick);
+        for (int i = 0; i < 7; ++i) cnt[i] += (need && i == pick);
     }
     return pick;
 }
@@ -1042,6 +1071,9 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     uint2 desc = make_uint2(0u, 0u);
     bool locknow = false;
     int32_t rew = 0;
+    // st_step's obs overlay of a spawn: its preview's descriptor, read in the
+    // action phase's LDS round trip (not on the store phase's chain)
+    [[maybe_unused]] uint2 pd_pv = make_uint2(0u, 0u);
     if constexpr (ACT) {
         // ---- action (tetris_env.py:245; value_action_map :152-160) + drop ----
         // Current and candidate descriptors and their columns are read in one
@@ -1051,6 +1083,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         const int cr = act == 4u ? ((rot + 1) & 3) : (act == 5u ? ((rot + 3) & 3) : rot);
         desc = tab(id * 4 + rot);
         const uint2 cdesc = tab(id * 4 + cr);
+        if constexpr (OVP && DO_L) pd_pv = tab(pv_id(mt0) * 4);
         uint32_t cur[4], cand[4];
         read_cols(L, lane, desc.y, ax, cur);
         read_cols(L, lane, cdesc.y, cx, cand);
@@ -1090,9 +1123,23 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     // before B1, so they arrive while it waits for the lock decision
     [[maybe_unused]] MtChunk chunk;
     [[maybe_unused]] MtRes mrs;
+    // ... and the count-dependent part of the preview draw (in st_step while
+    // the draw wave waits for the lock decision): a lane that draws spawns its
+    // preview first, so its draw sees the counts now + that shape (lanes
+    // without a valid preview redo this after their first draw, below)
+    [[maybe_unused]] int32_t cnt[7];
+    [[maybe_unused]] DrawPar dpar;
+    [[maybe_unused]] int32_t csid = 0;  // the spawned shape's count after the spawn
     if constexpr (DO_D) {
         mrs = mt_res(p.mt + e0 * kMtPitch, lane);
         mt_chunk_issue(mrs, mt0, real && !(kAblate & 2u), lane, chunk);
+        const int s0 = pv_id(mt0);
+#pragma unroll
+        for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)ss(ST_STAT_COUNT0 + i) + (i == s0);  // _new_piece :199
+        csid = cnt[0];
+#pragma unroll
+        for (int i = 1; i < 7; ++i) csid = s0 == i ? cnt[i] : csid;
+        dpar = draw_par(cnt);
     }
     if constexpr (TWO) {
         if constexpr (DO_L) {
@@ -1276,13 +1323,13 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             // or for a spawn its new piece at the spawn position -- the
             // preview, known since the step started, or (rare: no preview)
             // the draw wave's first draw, waited for here
-            int ps = pv_id(mt0);
+            // (the preview's descriptor was read with the action's)
+            uint2 pd = pd_pv;
             const bool need1 = draw && !pv_ok(mt0);
             if (__ballot(need1)) {
                 lds_flag_wait(&sm.f2, (uint32_t)t + 1u);
-                if (need1) ps = (int)sm.pick1[lane];
+                if (need1) pd = tab((int)sm.pick1[lane] * 4);
             }
-            const uint2 pd = tab(ps * 4);
             const uint32_t om = spawn ? pd.x : desc.x, og = spawn ? pd.y : desc.y;
             const int ox = spawn ? W / 2 : ax, oy = spawn ? 0 : ay;
 #pragma unroll
@@ -1359,9 +1406,6 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         // speculative in the draw wave (it does not know yet which locking
         // lanes die without auto-reset): committed below only where `draw`
         const bool dr_spec = TWO ? locknow : draw;
-        int32_t cnt[7];
-#pragma unroll
-        for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)ss(ST_STAT_COUNT0 + i);  // used by drawing lanes only
         if constexpr (STAMP) {  // diagnostic split of the draw: MT-word wait | compute
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             ST_STAMP(9);
@@ -1372,18 +1416,27 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             mt_win_consume<kWin>(pre);
             const bool need1 = dr_spec && !pv_ok(mt0);
             if (__ballot(need1)) {  // rare: after st_seed / st_mt_sync / a host-written state
-                const int pk = draw_shape<kWin, false>(need1, cnt, mtst, p.mt + e0 * kMtPitch, sm.S, lane, pre, false);
-                if (need1) sid = pk;
+                // the piece first, with the counts before the spawn
+                int32_t c0[7];
+#pragma unroll
+                for (int i = 0; i < 7; ++i) c0[i] = (int32_t)ss(ST_STAT_COUNT0 + i);
+                const int pk = draw_shape<kWin, false>(need1, c0, mtst, p.mt + e0 * kMtPitch, sm.S, lane, pre, false);
+                if (need1) {
+                    sid = pk;
+#pragma unroll
+                    for (int i = 0; i < 7; ++i) cnt[i] = c0[i] + (i == pk);  // _new_piece :199
+#pragma unroll
+                    for (int i = 0; i < 7; ++i) csid = pk == i ? cnt[i] : csid;
+                }
+                dpar = draw_par(cnt);
             }
             if constexpr (TWO) {
                 sm.pick1[lane] = (uint32_t)sid;
                 if (lane == 0) lds_flag_set(&sm.f2, (uint32_t)t + 1u);
             }
-#pragma unroll
-            for (int i = 0; i < 7; ++i) cnt[i] += (dr_spec && i == sid);  // _new_piece :199
             const uint32_t m0 = mtst;
-            const int npv = draw_shape<kWin, false>(dr_spec, cnt, mtst, p.mt + e0 * kMtPitch, sm.S, lane, pre,
-                                                    want_pre && pv_ok(mt0));
+            const int npv = draw_core<kWin>(dr_spec, dpar, mtst, p.mt + e0 * kMtPitch, sm.S, lane, pre,
+                                            want_pre && pv_ok(mt0));
             mt_new = pv_pack(mtst, npv, mt_consumed(m0, mtst));
         } else if constexpr (TWO) {
             sm.pick1[lane] = (uint32_t)sid;
@@ -1422,10 +1475,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             // st_step: this wave's changed counter rows straight from the
             // registers, one coalesced dword per lane and row (no staging
             // through LDS at the end of the chain): the MT word, and the
-            // count of the spawned shape (cnt[sid], already counted above)
-            int32_t csid = cnt[0];
-#pragma unroll
-            for (int i = 1; i < 7; ++i) csid = sid == i ? cnt[i] : csid;
+            // count of the spawned shape (csid, counted above)
             const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
             const uint32_t eo = (uint32_t)e * 4u;
             __builtin_amdgcn_raw_buffer_store_b32(
