@@ -210,6 +210,41 @@ def test_same_step_autoreset_equals_explicit_reset():
     assert np.array_equal(sa["stats"][:14], sb["stats"][:14])
 
 
+def test_reset_zeroes_host_written_holes_and_height():
+    """Default scoring flags (the kernel that never loads the old holes /
+    piece_height rows): host-written nonzero holes and heights survive locks
+    the reference's way (holes recounted at every lock, :278/:284; height
+    untouched, :289-292) and a same-step reset zeroes both like clear() (:308,
+    :310), i.e. exactly as 'none' + an explicit reset on the same stream."""
+    G = _engine()
+    n, T = 1024, 400
+    a = G.TetrisBatch(n, autoreset="none", seeds=range(n))
+    b = G.TetrisBatch(n, autoreset="same_step", seeds=range(n))
+    a.reset()
+    b.reset()
+    rng = np.random.default_rng(7)
+    st = a.get_state(("stats",))["stats"]
+    st[3] = rng.integers(0, 50, n)
+    st[4] = rng.integers(1, 20, n)
+    a.set_state(stats=st)
+    b.set_state(stats=st.copy())
+    died, mixed = 0, False
+    for t in range(T):
+        act = a.gen_actions(t, 11)
+        oa, ra, da = a.step(act)
+        oa, ra, da = oa.clone(), ra.clone(), da.clone()
+        ob, rb, db = b.step(act)
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db), t
+        if da.any():
+            died += int(da.sum())
+            a.reset(da.to(torch.uint8))
+        sa, sb = a.get_state(("stats",))["stats"], b.get_state(("stats",))["stats"]
+        assert np.array_equal(sa[:14], sb[:14]), t
+        # host-written heights kept through locks beside envs a reset zeroed
+        mixed |= bool((sb[4] != 0).any() and (sb[4] == 0).any())
+    assert died > 0 and mixed
+
+
 def test_sharding_invariance():
     """Envs keyed by global index: one batch of N == two shards of N/2."""
     G = _engine()
