@@ -135,6 +135,13 @@ constexpr int kNT = 2;
 #ifndef ST_LPRIO
 #define ST_LPRIO 0
 #endif
+// st_step's logic wave at issue priority 1 from its first instruction: since
+// the draw wave's parameters moved before B1 the logic wave's chain is the
+// step (A/B, 3 alternating rounds, K = 2,000: 4.67-4.72 -> 4.64-4.67 us,
+// steady burst 4.74-4.75 -> 4.68-4.71; profiles/r03/ab_step_lprio.txt)
+#ifndef ST_LPRIO0
+#define ST_LPRIO0 1
+#endif
 // st_step: the obs overlay goes to a plane of its own (OV), so the board and
 // obs rows are read in ONE transposed pass and stored together (A/B, 2 rounds
 // on one box, K = 2,000: 4.82-4.84 -> 4.80-4.81 us; tools/ab_step_libs.sh,
@@ -899,6 +906,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         tlast = __builtin_amdgcn_s_memtime();
     }
     ST_STAMP(0);
+    if constexpr (ROLE == kRoleL && KSTEPS == 1 && ST_LPRIO0 > 0) __builtin_amdgcn_s_setprio(ST_LPRIO0);
     uint32_t *const L = sm.L;
     uint32_t *const SS = sm.SS;
     const int W = WT ? WT : p.W;
