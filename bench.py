@@ -15,9 +15,11 @@ Envs auto-reset inside the step kernel when they die (the reference driver's
 processes itself (before anything touches a GPU) with the rendezvous on
 127.0.0.1; under torch.distributed.run it is one of the ranks.  Each rank owns
 a contiguous block of global env indices (seeds and actions keyed by the
-global index, so the work is identical at any N) and no collective runs in
-the timed steps ("scaling": "weak").  The RCCL gather of every shard's packed
-obs/reward/done to rank 0 (BASELINE config C5) is timed as `gather_variant`.
+global index, so the work is identical at any N; "scaling": "weak"), and each
+timed step is BASELINE config C5's step: st_step on every shard, then the
+RCCL gather of every shard's packed obs/reward/done to rank 0, double-buffered
+(step t+1 computes into the other buffer while the gather of step t runs).
+The same steps without the gather are reported beside it (`step_no_gather`).
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -276,7 +278,6 @@ def main():
     ap.add_argument("--no-surfaces", action="store_true",
                     help="skip the Python-surface timings (single_env, vec_env): PMC passes, whose "
                          "per-kernel averages would otherwise mix in their launches")
-    ap.add_argument("--gather-steps", type=int, default=200)
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -479,13 +480,87 @@ def main():
             """Steps t0 .. t1-1, one ctypes st_step call each."""
             fn, rc = self.fn, 0
             for a in self.args[t0:t1]:
-                rc |= fn(*a)
+                rc = rc or fn(*a)  # stop at the first failure and report its code
             C.check(rc)
 
         def warmup(self):
             with torch.cuda.stream(s):
                 self.launch_range(0, WU)
             torch.cuda.synchronize(dev)
+
+        # ---- BASELINE C5: every step's outputs gathered to rank 0 ----
+        def setup_gather(self):
+            """Two [W+2][n] output buffers (packed obs | reward | done, the
+            layout distributed.gather_outputs sends), rank 0's receive lists,
+            and the ctypes arguments of every step writing into buffer t % 2."""
+            self.nccl = args.backend == "nccl"
+            self.gbufs = [output_buffer(W, self.n_local, dev) for _ in range(2)]
+            views = [[ctypes.c_void_p(v.data_ptr()) for v in buffer_views(b, W)] for b in self.gbufs]
+            rdev = dev if self.nccl else torch.device("cpu")  # gloo gathers host tensors
+            self.grecv = [[torch.empty(b.shape, dtype=b.dtype, device=rdev) for _ in range(world)]
+                          if rank == 0 else None for b in self.gbufs]
+            ctx = self.eng._ctx
+            if self.f32:
+                self.gargs = [(ctx, self.aptr[t], views[t & 1][0], self.pf, views[t & 1][1], views[t & 1][2], sp)
+                              for t in range(WU + K)]
+            else:
+                self.gargs = [(ctx, self.aptr[t], *views[t & 1], sp) for t in range(WU + K)]
+            self.gworks = [None, None]
+            self.ngathers = 0
+
+        def gather_range(self, t0, t1):
+            """Steps t0 .. t1-1, each one st_step into buffer t % 2 and one
+            gather of that buffer to rank 0.  With RCCL the gather runs on
+            the collective's stream after the step (ProcessGroupNCCL orders
+            it behind the current stream, s), so step t+1 overlaps the gather
+            of step t; before step t+2 reuses a buffer, s waits for the gather
+            that read it.  All gathers are complete on s when this returns."""
+            fn, rc = self.fn, 0
+            for t in range(t0, t1):
+                k = t & 1
+                if self.gworks[k] is not None:
+                    self.gworks[k].wait()  # s (not the host) waits for the gather of step t - 2
+                rc = rc or fn(*self.gargs[t])
+                if self.nccl:
+                    self.gworks[k] = dist.gather(self.gbufs[k], gather_list=self.grecv[k], dst=0, async_op=True)
+                else:  # gloo: through host memory, no overlap
+                    s.synchronize()
+                    dist.gather(self.gbufs[k].cpu(), gather_list=self.grecv[k], dst=0)
+                self.ngathers += 1
+            for k in (0, 1):
+                if self.gworks[k] is not None:
+                    self.gworks[k].wait()
+                    self.gworks[k] = None
+            C.check(rc)
+
+        def measure_gather(self):
+            """C5's timed region: K x (st_step + gather to rank 0) after WU
+            such steps untimed.  Rank 0's assembled outputs of the last timed
+            step go to $ST_BENCH_DUMP (an .npz) when set (tests compare them
+            with the oracle)."""
+            self.setup_gather()
+            with torch.cuda.stream(s):
+                self.gather_range(0, WU)
+            torch.cuda.synchronize(dev)
+            g0 = self.ngathers
+            el, ev_ms, p_lock = timed(self.eng, lambda: self.gather_range(WU, WU + K), K)
+            ng = self.ngathers - g0
+            dump = os.environ.get("ST_BENCH_DUMP")
+            if rank == 0 and dump:
+                import numpy as np
+                from gym_simpletetris_amd.distributed import assemble
+                o, r, d = assemble([b.cpu() for b in self.grecv[(WU + K - 1) & 1]], W)
+                np.savez(dump, obs=o.numpy().view(np.uint32), reward=r.numpy(), done=d.numpy(),
+                         step=WU + K - 1, n_global=self.n_global, gathers_timed=ng)
+            bpr = self.gbufs[0].numel() * 4
+            ms = el / K * 1e3
+            return {"value": self.n_global * K / el, "ms_per_step": ms, "event_ms_per_step": ev_ms / K,
+                    "p_lock": p_lock, "gathers_timed": ng,
+                    "gather": {"backend": args.backend, "collective": "torch.distributed.gather to rank 0",
+                               "gathers_in_timed_region": ng, "bytes_per_rank_per_step": bpr,
+                               "bytes_into_rank0_per_step": bpr * (world - 1),
+                               "rank0_ingress_GBps": bpr * (world - 1) / (ms * 1e-3) / 1e9,
+                               "overlap": "double-buffered: step t+1 computes while step t is gathered"}}
 
         def runner(self):
             if args.launch == "eager":
@@ -542,7 +617,15 @@ def main():
     cfg_kw = CONFIGS[args.config]
     f32 = args.obs == "f32"
     head = Workload(args.n_envs, cfg_kw, f32)
-    hm = head.measure()
+    if use_dist:
+        # BASELINE C5: each timed step = st_step on every shard + the gather
+        # of its outputs to rank 0; the same steps without the gather beside it
+        gm = head.measure_gather()
+        ng = head.measure(steady=False)
+        hm = dict(gm, roofline=dict(ng["roofline"], note="st_step, the engine's kernel, from the "
+                                    "gather-free steps (step_no_gather); the gather's rate is in `gather`"))
+    else:
+        hm = head.measure()
     out = {
         "metric": METRIC,
         "value": hm["value"],
@@ -557,8 +640,12 @@ def main():
         "dtype": "u32",
         "data": "synthetic (uniform splitmix64 actions, seeds 1000 + global env index)",
         "config": {
-            "workload": f"{args.config.upper()}: {args.n_envs} parallel {W}x{H} boards per GPU, one "
-                        f"st_step per step, ram obs ({args.obs}), auto-reset, "
+            "workload": (f"C5: {head.n_global} boards sharded {args.n_envs} per GPU x {world}, one st_step per "
+                         f"shard per step + a gather of its packed obs/reward/done to rank 0 per step, "
+                         if use_dist else
+                         f"{args.config.upper()}: {args.n_envs} parallel {W}x{H} boards per GPU, one "
+                         f"st_step per step, ")
+                        + f"ram obs ({args.obs}), auto-reset, "
                         + ("advanced_clears+penalise_holes_increase+penalise_height_increase"
                            if args.config == "c4" else "default rewards"),
             "envs_per_gpu": args.n_envs,
@@ -575,6 +662,10 @@ def main():
         "event_ms_per_step": hm["event_ms_per_step"],
         "roofline": hm["roofline"],
     }
+    if use_dist:
+        out["gather"] = hm["gather"]
+        out["config"]["gathers_per_step"] = 1
+        out["step_no_gather"] = {k: ng[k] for k in ("value", "ms_per_step", "event_ms_per_step", "p_lock")}
 
     if not args.no_extras:
         variants = {}
@@ -637,9 +728,6 @@ def main():
                                                        kname_of, dev, s, sp, rank, world, W, H, K, WU,
                                                        aseed, args.config, args.launch)
         out["variants"] = variants
-        if use_dist:
-            out["gather_variant"] = gather_variant(head, args, C, output_buffer, buffer_views,
-                                                   dev, s, sp, rank, world, W, WU, max_over_ranks)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.config)
     if rank == 0:
@@ -807,52 +895,6 @@ def clear_heavy(head, cfg_kw, C, ShardedTetris, timed, roofline, kname_of, dev, 
     del g
     ce.close()
     return r
-
-
-def gather_variant(head, args, C, output_buffer, buffer_views, dev, s, sp, rank, world, W, WU,
-                   max_over_ranks):
-    """BASELINE config C5's exchange: each step's packed obs/reward/done of
-    every shard gathered to rank 0 (torch.distributed.gather; RCCL over xGMI
-    with the nccl backend).  Double-buffered: the gather of step t runs on the
-    collective stream while step t+1 computes into the other buffer."""
-    G = min(args.gather_steps, args.steps)
-    eng = head.eng
-    L, ctx = eng._L, eng._ctx
-    n = head.n_local
-    nccl = args.backend == "nccl"
-    bufs = [output_buffer(W, n, dev) for _ in range(2)]
-    views = [[ctypes.c_void_p(v.data_ptr()) for v in buffer_views(b, W)] for b in bufs]
-    recv = [[torch.empty_like(b) for _ in range(world)] if rank == 0 else None for b in bufs]
-    if not nccl:  # gloo: host tensors, no overlap
-        recv = [[torch.empty_like(b, device="cpu") for _ in range(world)] if rank == 0 else None
-                for b in bufs]
-    torch.cuda.synchronize(dev)
-    dist.barrier()
-    t0 = time.perf_counter()
-    works = [None, None]
-    for i in range(G):
-        k = i & 1
-        with torch.cuda.stream(s):
-            if works[k] is not None:
-                works[k].wait()  # s waits for the gather that still reads bufs[k]
-            C.check(L.st_step(ctx, head.aptr[WU + i], *views[k], sp))
-            if nccl:
-                works[k] = dist.gather(bufs[k], gather_list=recv[k], dst=0, async_op=True)
-            else:
-                s.synchronize()
-                dist.gather(bufs[k].cpu(), gather_list=recv[k], dst=0)
-    with torch.cuda.stream(s):
-        for w in works:
-            if w is not None:
-                w.wait()
-    torch.cuda.synchronize(dev)
-    dist.barrier()
-    gdt = max_over_ranks(time.perf_counter() - t0)
-    return {"value": head.n_global * G / gdt, "ms_per_step": gdt / G * 1e3, "steps": G,
-            "bytes_per_rank_per_step": bufs[0].numel() * 4,
-            "backend": args.backend,
-            "note": "eager st_step + gather of packed obs/reward/done to rank 0 every step, "
-                    "double-buffered so step t+1 overlaps the gather of step t"}
 
 
 if __name__ == "__main__":

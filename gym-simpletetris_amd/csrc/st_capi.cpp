@@ -189,7 +189,8 @@ int st_reset(st_ctx *c, const uint8_t *d_mask, st_stream stream) {
 }
 
 static int step_impl(st_ctx *c, const uint8_t *d_actions, uint32_t *d_obs, float *d_obs_f32,
-                     int32_t *d_reward, uint8_t *d_done, st_stream stream) {
+                     int32_t *d_reward, uint8_t *d_done, st_stream stream, uint32_t *d_final_obs = nullptr,
+                     int32_t *d_info = nullptr) {
     if (!c || !d_actions) return fail(ST_EINVAL, "st_step: null argument");
     if (!c->seeded || !c->reset_once)
         return fail(ST_ESTATE, "st_step before st_seed + st_reset (tetris_env.py:244 needs an anchor)");
@@ -200,6 +201,8 @@ static int step_impl(st_ctx *c, const uint8_t *d_actions, uint32_t *d_obs, float
     p.obs_f32 = d_obs_f32;
     p.reward = d_reward;
     p.done = d_done;
+    p.final_obs = d_final_obs;
+    p.info = d_info;
     ST_HIP(st::launch_step(p, (hipStream_t)stream));
     return ST_OK;
 }
@@ -213,6 +216,11 @@ int st_step_f32(st_ctx *c, const uint8_t *d_actions, uint32_t *d_obs, float *d_o
                 int32_t *d_reward, uint8_t *d_done, st_stream stream) {
     if (!d_obs_f32) return fail(ST_EINVAL, "st_step_f32: null d_obs_f32");
     return step_impl(c, d_actions, d_obs, d_obs_f32, d_reward, d_done, stream);
+}
+
+int st_step_vec(st_ctx *c, const uint8_t *d_actions, uint32_t *d_obs, float *d_obs_f32, int32_t *d_reward,
+                uint8_t *d_done, uint32_t *d_final_obs, int32_t *d_info, st_stream stream) {
+    return step_impl(c, d_actions, d_obs, d_obs_f32, d_reward, d_done, stream, d_final_obs, d_info);
 }
 
 int st_rollout(st_ctx *c, int32_t k, const uint8_t *d_actions, uint32_t *d_obs, float *d_obs_f32,

@@ -55,6 +55,8 @@ struct KParams {
     int32_t *reward;         // [n]
     uint8_t *done;           // [n]
     uint32_t *act_flag;      // st_set_action_flag: sticky "action outside 0..6" word, or null
+    uint32_t *final_obs;     // st_step_vec: [W][n] terminal obs of envs reset in the step, or null
+    int32_t *info;           // st_step_vec: [ST_NSTAT][n] counters after the step, or null
     int32_t cus;             // compute units of the device (launch_rollout's kernel choice)
 };
 

@@ -880,8 +880,15 @@ __device__ __forceinline__ void lds_flag_wait_ge(uint32_t *f, uint32_t v) {
 // tetris_env.py:126-137): those tests fold away at compile time (measured:
 // the rollout loop otherwise holds each flag as a 64-bit lane mask at the
 // SGPR limit, -5% packed rollout; st_step -1%).
-template <int WT, int HT, bool F32, bool STAMP, int KSTEPS, bool SC0, int ROLE>
+// VEC (st_step_vec, two-wave st_step only): the vector env's outputs -- with
+// p.final_obs, an env reset in this step returns the reset obs (the empty
+// board clear() returns, tetris_env.py:306-315, :405-411) and its terminal
+// obs goes to final_obs; with p.info, every counter row after the step is
+// written to info [ST_NSTAT][n] (the ep_* rows: the finished episode's where
+// the env was reset, else 0).
+template <int WT, int HT, bool F32, bool STAMP, int KSTEPS, bool SC0, int ROLE, bool VEC = false>
 __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KSTEPS> &sm) {
+    static_assert(!VEC || (KSTEPS == 1 && ROLE != kRoleOne), "VEC: the two-wave st_step only");
     constexpr bool DO_L = ROLE != kRoleD;  // action, lock path, outputs
     constexpr bool DO_D = ROLE != kRoleL;  // MT words, next-generation block, draws
     constexpr bool TWO = ROLE != kRoleOne;
@@ -1362,7 +1369,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         const auto rb = buf_rsrc(p.board, (uint32_t)W * (uint32_t)sd * 4u);
         const uint32_t boff = ((uint32_t)e0 * 4u + loff * 4u);
         const bool wide_obs1 = OVP && (p.n & 3) == 0 && e0 + kWave <= p.n &&
-                               (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0;
+                               (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0 &&
+                               (!VEC || (reinterpret_cast<uintptr_t>(p.final_obs) & 15u) == 0);
 #pragma unroll
         for (int q = 0; q < NBQ; ++q) {
             if (WT || 4 * q < W) {
@@ -1372,9 +1380,20 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                         const uint4 o = ow[q];
                         const uint4 ob = make_uint4((v.x | o.x) & hmask, (v.y | o.y) & hmask, (v.z | o.z) & hmask,
                                                     (v.w | o.w) & hmask);
-                        buf_store16<kNT>(buf_rsrc(p.obs, (uint32_t)W * (uint32_t)p.n * 4u),
-                                         ((uint32_t)e0 + (uint32_t)(4 * q + lrow) * (uint32_t)p.n + (uint32_t)lcc) * 4u,
-                                         ob);
+                        const uint32_t ooff =
+                            ((uint32_t)e0 + (uint32_t)(4 * q + lrow) * (uint32_t)p.n + (uint32_t)lcc) * 4u;
+                        if constexpr (VEC) {
+                            // reset envs (km = 0): the reset obs here, the
+                            // terminal one to final_obs (groups with a reset)
+                            const bool fin = p.final_obs && !(km.x && km.y && km.z && km.w);
+                            buf_store16<kNT>(buf_rsrc(p.final_obs, (uint32_t)W * (uint32_t)p.n * 4u),
+                                             fin ? ooff : kOff, ob);
+                            const uint4 keep = p.final_obs ? km : make_uint4(~0u, ~0u, ~0u, ~0u);
+                            buf_store16<kNT>(buf_rsrc(p.obs, (uint32_t)W * (uint32_t)p.n * 4u), ooff,
+                                             make_uint4(ob.x & keep.x, ob.y & keep.y, ob.z & keep.z, ob.w & keep.w));
+                        } else {
+                            buf_store16<kNT>(buf_rsrc(p.obs, (uint32_t)W * (uint32_t)p.n * 4u), ooff, ob);
+                        }
                     }
                 }
                 v.x &= km.x;
@@ -1490,6 +1509,14 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 mt_out, rs, dr || chunk_me ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff, 0, kNT);
             __builtin_amdgcn_raw_buffer_store_b32(
                 (uint32_t)csid, rs, dr ? eo + (uint32_t)(ST_STAT_COUNT0 + sid) * (uint32_t)sd * 4u : kOff, 0, kNT);
+            if constexpr (VEC) {  // st_step_vec's info snapshot: the shape counts after the step
+                const auto ri = buf_rsrc(p.info, (uint32_t)ST_NSTAT * (uint32_t)p.n * 4u);
+#pragma unroll
+                for (int i = 0; i < 7; ++i)
+                    __builtin_amdgcn_raw_buffer_store_b32(
+                        (uint32_t)(dr ? cnt[i] : (int32_t)ss(ST_STAT_COUNT0 + i)), ri,
+                        real ? ((uint32_t)(ST_STAT_COUNT0 + i) * (uint32_t)p.n + (uint32_t)e) * 4u : kOff, 0, kNT);
+            }
         } else {
             if (dr || chunk_me) {
                 ss(ST_STAT_MT_INDEX) = mt_out;
@@ -1532,6 +1559,15 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         }
 
         // ---- counters back to the staged rows (tetris_env.py:253, :264-299) ----
+        [[maybe_unused]] int32_t ep_t = 0, ep_s = 0, ep_l = 0, ep_h = 0;  // VEC: info's ep_* rows
+        if constexpr (VEC) {
+            if (reset_now) {
+                ep_t = time;
+                ep_s = score;
+                ep_l = lines;
+                ep_h = holes;
+            }
+        }
         if (reset_now) {  // the finished episode's counters (ST_AUTORESET_SAME_STEP)
             int32_t *st = p.stats + e;
             st[ST_STAT_EP_TIME * sd] = time;
@@ -1560,6 +1596,27 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             put(ST_STAT_HOLES, holes, locknow && holes != o_holes);
             put(ST_STAT_PIECE_HEIGHT, height, locknow && height != o_height);
             put(ST_STAT_DEATHS, deaths, locknow && deaths != o_deaths);
+            if constexpr (VEC) {
+                // st_step_vec's info snapshot: this wave's rows for every env
+                // (locking lanes from the registers, the others unchanged)
+                const auto ri = buf_rsrc(p.info, (uint32_t)ST_NSTAT * (uint32_t)p.n * 4u);
+                const uint32_t io = (uint32_t)e * 4u;
+                auto inf = [&](int r, int32_t v) {
+                    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, ri, real ? io + (uint32_t)r * (uint32_t)p.n * 4u : kOff,
+                                                          0, kNT);
+                };
+                inf(ST_STAT_TIME, time);
+                inf(kPieceRow, (int32_t)pw_out);
+                inf(ST_STAT_SCORE, locknow ? score : (int32_t)ss(ST_STAT_SCORE));
+                inf(ST_STAT_LINES, locknow ? lines : (int32_t)ss(ST_STAT_LINES));
+                inf(ST_STAT_HOLES, locknow ? holes : (int32_t)ss(ST_STAT_HOLES));
+                inf(ST_STAT_PIECE_HEIGHT, locknow ? height : (int32_t)ss(ST_STAT_PIECE_HEIGHT));
+                inf(ST_STAT_DEATHS, locknow ? deaths : (int32_t)ss(ST_STAT_DEATHS));
+                inf(ST_STAT_EP_TIME, ep_t);
+                inf(ST_STAT_EP_SCORE, ep_s);
+                inf(ST_STAT_EP_LINES, ep_l);
+                inf(ST_STAT_EP_HOLES, ep_h);
+            }
         } else {
             ss(ST_STAT_TIME) = (uint32_t)time;
             ss(kPieceRow) = pw_out;
@@ -1583,7 +1640,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         }
         wave_sync();
         const bool wide_obs = (p.n & 3) == 0 && e0 + kWave <= p.n &&
-                              (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0;
+                              (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0 &&
+                              (!VEC || (reinterpret_cast<uintptr_t>(p.final_obs) & 15u) == 0);
         if (obs_t && !(kAblate & 8u)) {
             if (OVP && wide_obs) {
                 // stored with the board rows
@@ -1604,10 +1662,17 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 }
             } else if (real) {  // ragged / unaligned: one dword per row, 32-bit offsets (SGPRs)
                 const auto ro = buf_rsrc(obs_t, (uint32_t)W * (uint32_t)p.n * 4u);
+                // VEC with final_obs: a reset env returns the reset obs, its
+                // terminal obs goes to final_obs
+                const bool fin = VEC && p.final_obs && reset_now;
+                const auto rf = buf_rsrc(VEC ? p.final_obs : nullptr, (uint32_t)W * (uint32_t)p.n * 4u);
 #pragma unroll 1
-                for (int x = 0; x < W; ++x)
-                    __builtin_amdgcn_raw_buffer_store_b32((lcol(L, x, lane) | (OVP ? lcol(sm.OV, x, lane) : 0u)) & hmask,
-                                                          ro, ((uint32_t)x * (uint32_t)p.n + (uint32_t)e) * 4u, 0, kNT);
+                for (int x = 0; x < W; ++x) {
+                    const uint32_t v = (lcol(L, x, lane) | (OVP ? lcol(sm.OV, x, lane) : 0u)) & hmask;
+                    const uint32_t off = ((uint32_t)x * (uint32_t)p.n + (uint32_t)e) * 4u;
+                    __builtin_amdgcn_raw_buffer_store_b32(fin ? 0u : v, ro, off, 0, kNT);
+                    if constexpr (VEC) __builtin_amdgcn_raw_buffer_store_b32(v, rf, fin ? off : kOff, 0, kNT);
+                }
             }
         }
         if (F32) {
@@ -1621,9 +1686,11 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 // the column word; the float4 comes from the 16-entry table.
                 constexpr int CPC = HT / 4, CPE = WT * CPC;
                 uint32_t *O = sm.O;
+                // (VEC with final_obs: a reset env's float32 obs is the reset obs)
+                const uint32_t omask = VEC && p.final_obs && reset_now ? 0u : hmask;
 #pragma unroll
                 for (int x = 0; x < WT; ++x)
-                    O[lane * (WT + 1) + x] = (lcol(L, x, lane) | (OVP ? lcol(sm.OV, x, lane) : 0u)) & hmask;
+                    O[lane * (WT + 1) + x] = (lcol(L, x, lane) | (OVP ? lcol(sm.OV, x, lane) : 0u)) & omask;
                 wave_sync();
                 float4 *out4 = reinterpret_cast<float4 *>(out);
                 const float4 *F4 = reinterpret_cast<const float4 *>(sm.F4);
@@ -1649,8 +1716,10 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             } else {
                 const int per_env = W * H;
                 const int total = nreal * per_env;
+                // (VEC with final_obs: KM[ee] = 0 for a reset env -- its reset obs)
                 auto word = [&](int ee, int x) {
-                    return (L[(x + kPad) * kWave + ee] | (OVP ? sm.OV[(x + kPad) * kWave + ee] : 0u)) & hmask;
+                    return (L[(x + kPad) * kWave + ee] | (OVP ? sm.OV[(x + kPad) * kWave + ee] : 0u)) &
+                           (VEC && p.final_obs ? sm.KM[ee] : hmask);
                 };
                 for (int f = lane; f < total; f += kWave) {
                     const int ee = f / per_env;
@@ -1765,11 +1834,11 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
 }
 
 // st_step: two waves per 64 envs (kRoleL, kRoleD), see run_steps.
-template <int WT, int HT, bool F32, bool STAMP = false, bool SC0 = false>
+template <int WT, int HT, bool F32, bool STAMP = false, bool SC0 = false, bool VEC = false>
 __global__ __launch_bounds__(2 * kWave) void k_step(KParams p) {
     __shared__ StepLds<WT, F32, 1> sm;
-    if (threadIdx.x < kWave) run_steps<WT, HT, F32, STAMP, 1, SC0, kRoleL>(p, sm);
-    else run_steps<WT, HT, F32, STAMP, 1, SC0, kRoleD>(p, sm);
+    if (threadIdx.x < kWave) run_steps<WT, HT, F32, STAMP, 1, SC0, kRoleL, VEC>(p, sm);
+    else run_steps<WT, HT, F32, STAMP, 1, SC0, kRoleD, VEC>(p, sm);
 }
 
 // ---------------------------------------------------------------- rollout
@@ -3380,7 +3449,17 @@ hipError_t launch_step(const KParams &p, hipStream_t s) {
     const dim3 grid((unsigned)(p.stride / kWave)), block(2 * kWave);  // logic + draw wave
     const bool f32 = p.obs_f32 != nullptr;
     const bool sc0 = !(p.flags & kScoringFlags);
-    if (p.stamps && p.W == 10 && p.H == 20) {
+    if (p.final_obs || p.info) {  // st_step_vec: the vector env's outputs (VEC)
+        if (p.W == 10 && p.H == 20) {
+            if (f32 && sc0) hipLaunchKernelGGL((k_step<10, 20, true, false, true, true>), grid, block, 0, s, p);
+            else if (f32) hipLaunchKernelGGL((k_step<10, 20, true, false, false, true>), grid, block, 0, s, p);
+            else if (sc0) hipLaunchKernelGGL((k_step<10, 20, false, false, true, true>), grid, block, 0, s, p);
+            else hipLaunchKernelGGL((k_step<10, 20, false, false, false, true>), grid, block, 0, s, p);
+        } else {
+            if (f32) hipLaunchKernelGGL((k_step<0, 0, true, false, false, true>), grid, block, 0, s, p);
+            else hipLaunchKernelGGL((k_step<0, 0, false, false, false, true>), grid, block, 0, s, p);
+        }
+    } else if (p.stamps && p.W == 10 && p.H == 20) {
         if (f32) hipLaunchKernelGGL((k_step<10, 20, true, true>), grid, block, 0, s, p);
         else if (sc0) hipLaunchKernelGGL((k_step<10, 20, false, true, true>), grid, block, 0, s, p);
         else hipLaunchKernelGGL((k_step<10, 20, false, true>), grid, block, 0, s, p);

@@ -36,7 +36,7 @@ NSTAT = 19
 MT_N = 624
 EXPORT_MT, EXPORT_OBS_F32 = 1, 2  # st_export_env parts
 
-EXPORTS = ("st_create", "st_destroy", "st_seed", "st_reset", "st_step", "st_step_f32", "st_rollout",
+EXPORTS = ("st_create", "st_destroy", "st_seed", "st_reset", "st_step", "st_step_f32", "st_step_vec", "st_rollout",
            "st_obs_to_f32", "st_render", "st_grayscale", "st_state", "st_copy", "st_mt_sync", "st_state_bytes", "st_save",
            "st_load", "st_export_env", "st_export_words", "st_check_actions", "st_set_action_flag", "st_stream_sync",
            "st_host_device_ptr", "st_gen_actions", "st_policy_greedy", "st_debug_stamps", "st_last_error", "st_abi_version")
@@ -86,6 +86,7 @@ def load(path: str = LIB_PATH):
         "st_reset": ([vp, vp, vp], ctypes.c_int),
         "st_step": ([vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "st_step_f32": ([vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
+        "st_step_vec": ([vp, vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "st_rollout": ([vp, i32, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "st_obs_to_f32": ([vp, vp, vp, vp], ctypes.c_int),
         "st_render": ([vp, vp, vp], ctypes.c_int),

@@ -236,10 +236,14 @@ class TetrisBatch:
                 if bool(bad.any()):
                     v = x[bad].flatten()[0].item()
                     raise KeyError(f"action {v} not in 0..6 (tetris_env.py:245)")
-            elif asyn and x.dtype != torch.uint8:  # keep bad values visible to the kernel's check
-                x = torch.where(_bad_actions(x), torch.full_like(x, 255), x)
-            t = x if (x.dtype == torch.uint8 and x.device == self.device) \
-                else x.to(device=self.device).to(torch.uint8)
+            if x.dtype == torch.uint8 and x.device == self.device:
+                t = x
+            else:
+                t = x.to(device=self.device).to(torch.uint8)
+                if asyn:  # keep bad values visible to the kernel's check: a cast may wrap them
+                    # into 0..6 (int16 256 -> 0, 2.5 -> 2); the sentinel is set after the cast,
+                    # in uint8, so no source dtype has to hold 255 (int8 cannot)
+                    t = t.masked_fill_(_bad_actions(x).to(self.device), 255)
             return t.reshape(shape).contiguous()
         a = np.asarray(x)
         if a.size != int(np.prod(shape)):

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes
 import random
+import weakref
 from typing import Optional
 
 import numpy as np
@@ -290,30 +291,78 @@ class TetrisEnv:
             self.engine = None
 
 
-class VecInfo:
-    """get_info() (tetris_env.py:232-241) for N envs as int32 GPU tensors.
-    The counters are snapshotted (one device-to-device copy on the step's
-    stream) when step() returns, so an info kept past later steps still
-    describes its own step; the per-key tensors are built on first access."""
+class _Slot:
+    """One set of st_step_vec outputs (the vector env alternates two)."""
 
-    def __init__(self, engine: TetrisBatch):
-        self._engine = engine
-        self._stats = engine.state_tensors(("stats",), sync=False)["stats"]
+    def __init__(self, n, width, height, dev, f32, final):
+        self.obs = torch.zeros((width, n), dtype=torch.int32, device=dev)
+        self.obs_f32 = torch.zeros((n, width, height), dtype=torch.float32, device=dev) if f32 else None
+        self.reward = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.done = torch.zeros(n, dtype=torch.bool, device=dev)
+        self.final = torch.zeros((width, n), dtype=torch.int32, device=dev) if final else None
+        self.info = torch.zeros((C.NSTAT, n), dtype=torch.int32, device=dev)
+        self.ptrs = tuple(None if t is None else ctypes.c_void_p(t.data_ptr()) for t in
+                          (self.obs, self.obs_f32, self.reward, self.done, self.final, self.info))
+        self.owner = None  # weakref to the VecInfo that reads this slot
+
+
+class VecInfo:
+    """get_info() (tetris_env.py:232-241) of one TetrisVecEnv step for all N
+    envs, as int32 GPU tensors built on first access: time, score,
+    lines_cleared, holes, deaths, piece_height, current_piece (shape id, the
+    index into SHAPE_NAMES), statistics [7, N]; ep_time / ep_score /
+    ep_lines / ep_holes (the finished episode's counters where the env was
+    reset in this step, else 0); and, with the gym reset convention,
+    final_observation (the terminal obs of the envs reset in this step, in
+    the env's obs format; zeros elsewhere) and _final_observation (bool [N],
+    which envs those are).
+
+    The step kernel writes the counters into the slot this info reads, so
+    building it costs nothing per step; the env reuses a slot two steps later
+    and copies it into this object first if this info is still alive then."""
+
+    def __init__(self, env: "TetrisVecEnv", slot: _Slot):
+        self._env = env
+        self._info, self._final, self._done = slot.info, slot.final, slot.done
         self._cache = None
+
+    def _detach(self):
+        """Own copies of the slot's tensors (the env is about to reuse it;
+        stream-ordered before the step that overwrites it)."""
+        self._info = self._info.clone()
+        self._done = self._done.clone()
+        if self._final is not None:
+            self._final = self._final.clone()
 
     def _load(self):
         if self._cache is None:
-            self._cache = self._engine.info_tensors(self._stats)
+            env = self._env
+            d = env.engine.info_tensors(self._info)
+            d["current_piece"] = self._info[C.STAT["piece"]] & 7
+            if self._final is not None:
+                fin = torch.where(self._done.unsqueeze(0), self._final, torch.zeros_like(self._final))
+                d["final_observation"] = env._obs(fin, None)
+                d["_final_observation"] = self._done.clone()
+            self._cache = d
         return self._cache
 
     def __getitem__(self, k):
         return self._load()[k]
 
+    def get(self, k, default=None):
+        return self._load().get(k, default)
+
     def keys(self):
         return self._load().keys()
 
+    def items(self):
+        return self._load().items()
+
     def __contains__(self, k):
         return k in self._load()
+
+    def __iter__(self):
+        return iter(self._load())
 
 
 class TetrisVecEnv:
@@ -324,18 +373,28 @@ class TetrisVecEnv:
            [N, 84, 84(, 1|3)] for 'grayscale' / 'rgb', or the packed uint32
            [W, N] words with obs_format='packed'.
     With autoreset=True (default) envs that died are reset inside the same
-    kernel (TetrisEngine.clear); the returned obs of such an env is its
-    terminal observation (what the reference's step returned) and
+    kernel (TetrisEngine.clear).  autoreset_obs='reset' (default; gym's
+    vector-env convention): the returned obs of such an env is
+    its RESET obs -- the empty board clear() returns (tetris_env.py:306-315,
+    :405-411) -- and its terminal observation (what the reference's step
+    returned) is in info['final_observation'] (materialised on first access,
+    valid where info['_final_observation']); 'terminal': the returned obs is
+    the terminal observation itself (no final_observation key).
     info['ep_score'] / ['ep_lines'] / ['ep_time'] / ['ep_holes'] hold the
-    finished episode's counters.  Buffers are reused between steps.
+    finished episode's counters.  One st_step_vec launch per step writes the
+    obs, reward, done, the terminal obs and the info counters; the returned
+    tensors live in one of two output slots that alternate, so they stay
+    valid until two steps later (an info object kept longer takes a copy).
     Actions outside 0..6 raise KeyError like the reference's.  By default
     (`validate_actions='async'`) the step kernel checks the actions it loads
     anyway and sets a sticky flag in mapped host memory: no extra launch and
-    no sync, the KeyError comes at the next step() after the flag is seen or
-    from check_actions().  `validate_actions=True` checks before the step
-    (the reference's immediate KeyError; for actions already on the GPU one
-    device->host sync per step); `False` does not check (out-of-range values
-    act as idle).  Host (numpy / list) actions are always checked up front.
+    no sync; the flagged step has already been applied with the bad action
+    acting as idle, and the KeyError comes at the next step() after the flag
+    is seen or from check_actions().  `validate_actions=True` checks before
+    the step (the reference's immediate KeyError, before any state changes;
+    for actions already on the GPU one device->host sync per step); `False`
+    does not check (out-of-range values act as idle).  Host (numpy / list)
+    actions are always checked up front.
     """
 
     def __init__(self, num_envs: int, width=10, height=20, obs_type="ram", extend_dims=False,
@@ -343,12 +402,15 @@ class TetrisVecEnv:
                  advanced_clears=False, high_scoring=False, penalise_holes=False,
                  penalise_holes_increase=False, lock_delay=0, step_reset=False, *,
                  device=None, seed: int = 0, global_offset: int = 0, autoreset: bool = True,
-                 obs_format: str = "f32", validate_actions="async"):
+                 autoreset_obs: str = "reset", obs_format: str = "f32", validate_actions="async"):
         if obs_format not in ("f32", "packed"):
             raise ValueError("obs_format must be 'f32' or 'packed'")
+        if autoreset_obs not in ("reset", "terminal"):
+            raise ValueError("autoreset_obs must be 'reset' (gym's convention) or 'terminal'")
         self.num_envs = int(num_envs)
         self.width, self.height = width, height
         self.obs_type, self.extend_dims, self.obs_format = obs_type, extend_dims, obs_format
+        self.autoreset, self.autoreset_obs = bool(autoreset), autoreset_obs
         self.engine = TetrisBatch(self.num_envs, width=width, height=height,
                                   lock_delay=lock_delay, step_reset=step_reset,
                                   reward_step=reward_step, penalise_height=penalise_height,
@@ -362,6 +424,11 @@ class TetrisVecEnv:
         self.single_action_space = spaces.Discrete(7)
         self.single_observation_space = _obs_space(obs_type, width, height, extend_dims)
         self.device = self.engine.device
+        self._want_f32 = obs_format == "f32" and obs_type == "ram"
+        fin = self.autoreset and autoreset_obs == "reset"
+        self._slots = [_Slot(self.num_envs, width, height, self.device, self._want_f32, fin) for _ in range(2)]
+        self._k = 0
+        self._step_vec = self.engine._L.st_step_vec
 
     def _obs(self, packed, f32):
         if self.obs_format == "packed":
@@ -382,10 +449,19 @@ class TetrisVecEnv:
                                             device=self.device) if self.obs_type == "ram" else None)
 
     def step(self, actions):
-        want_f32 = self.obs_format == "f32" and self.obs_type == "ram"
-        out = self.engine.step(actions, obs="f32" if want_f32 else "packed")
-        f32 = out[0] if want_f32 else None
-        return self._obs(self.engine.obs, f32), out[1], out[2], VecInfo(self.engine)
+        eng = self.engine
+        a = eng._actions(actions)
+        slot = self._slots[self._k]
+        self._k ^= 1
+        held = slot.owner() if slot.owner is not None else None
+        if held is not None:  # an info from two steps ago is still alive: it keeps a copy
+            held._detach()
+        po, pf, pr, pd, pfin, pinfo = slot.ptrs
+        C.check(self._step_vec(eng._ctx, ctypes.c_void_p(a.data_ptr()), po, pf, pr, pd, pfin, pinfo,
+                               eng._stream()))
+        info = VecInfo(self, slot)
+        slot.owner = weakref.ref(info)
+        return self._obs(slot.obs, slot.obs_f32), slot.reward, slot.done, info
 
     def check_actions(self):
         """validate_actions='async': raise KeyError if an action outside 0..6

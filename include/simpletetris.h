@@ -150,6 +150,28 @@ int st_step(st_ctx *ctx, const uint8_t *d_actions, uint32_t *d_obs, int32_t *d_r
 int st_step_f32(st_ctx *ctx, const uint8_t *d_actions, uint32_t *d_obs, float *d_obs_f32,
                 int32_t *d_reward, uint8_t *d_done, st_stream stream);
 
+/* st_step for a vector env (gym's autoreset convention), one
+ * launch.  d_obs_f32 may be NULL (packed only).
+ *   d_final_obs (uint32 [width][n_envs], or NULL): when given, an env that
+ *     died and was reset inside this step (ST_AUTORESET_SAME_STEP) returns
+ *     the RESET observation in d_obs / d_obs_f32 -- the empty board that
+ *     clear() returns (tetris_env.py:306-315, :405-411) -- and its terminal
+ *     observation (what the reference's step returned, :301-302) is written
+ *     to d_final_obs.  Only the columns of such envs are meaningful (the
+ *     kernel writes 16-B groups holding one).  NULL: the terminal obs is
+ *     returned in d_obs (st_step's convention).
+ *   d_info (int32 [ST_NSTAT][n_envs], or NULL): every counter row after the
+ *     step (get_info, :232-241, from one snapshot written by the step
+ *     kernel): rows ST_STAT_* as in st_state_views.stats except
+ *     ST_STAT_MT_INDEX (not written); the ST_STAT_EP_* rows hold the
+ *     finished episode's counters where the env was reset in this step and
+ *     0 elsewhere.
+ * The headline st_step kernel is a separate instantiation: these outputs
+ * cost it nothing. */
+int st_step_vec(st_ctx *ctx, const uint8_t *d_actions, uint32_t *d_obs, float *d_obs_f32,
+                int32_t *d_reward, uint8_t *d_done, uint32_t *d_final_obs, int32_t *d_info,
+                st_stream stream);
+
 /* k consecutive st_step calls in ONE launch: the driver loop of README.md:43-51
  * (`for t: obs, r, done, info = env.step(a[t])`) with all actions known up
  * front (synthetic / replayed rollouts).  Boards and counters stay on chip

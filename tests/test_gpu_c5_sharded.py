@@ -161,21 +161,28 @@ def test_c5_eight_ranks_ragged(tmp_path):
 
 
 @pytest.mark.timeout(400)
-def test_bench_gpus8_direct_invocation():
+def test_bench_gpus8_direct_invocation(tmp_path):
     """`python bench.py --gpus 8` run directly: it spawns its 8 ranks itself
-    (the driver's C5 launch path, here all on cuda:0 over gloo), they time
-    their shards, the gather variant runs, rank 0 prints one JSON line."""
-    env = dict(os.environ, ST_BENCH_SHARED_GPU="1")
+    (the driver's C5 launch path, here all on cuda:0 over gloo); every timed
+    step is st_step on each shard + the gather to rank 0 (K gathers inside
+    the region), and rank 0's assembled outputs of the last timed step equal
+    the oracle stepping all 8 x 2,048 envs.  Rank 0 prints one JSON line."""
+    from test_gpu_multirank import check_bench_dump
+    dump = tmp_path / "c5.npz"
+    env = dict(os.environ, ST_BENCH_SHARED_GPU="1", ST_BENCH_DUMP=str(dump))
     env.pop("WORLD_SIZE", None)
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--backend", "gloo",
                         "--steps", "20", "--warmup", "5", "--n-envs", "2048", "--no-cpu-baseline",
-                        "--no-clear-heavy", "--no-surfaces", "--gather-steps", "10"],
+                        "--no-clear-heavy", "--no-surfaces"],
                        env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1  # rank 0 prints one JSON line
     d = json.loads(lines[0])
     assert d["n_gpus"] == 8 and d["config"]["envs_total"] == 8 * 2048
-    assert d["value"] > 0 and d["gather_variant"]["steps"] == 10
-    assert d["gather_variant"]["bytes_per_rank_per_step"] == (10 + 2) * 2048 * 4
+    assert d["value"] > 0 and d["gather"]["gathers_in_timed_region"] == 20
+    assert d["gather"]["bytes_per_rank_per_step"] == (10 + 2) * 2048 * 4
+    assert d["config"]["workload"].startswith("C5:")
     assert d["scaling"] == "weak"
+    z = check_bench_dump(dump, 8 * 2048, 25)
+    assert int(z["gathers_timed"]) == 20

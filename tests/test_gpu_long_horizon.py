@@ -53,13 +53,13 @@ class ParallelOracle:
             ob.reset()
         self.pool = ThreadPoolExecutor(len(self.sl))
 
-    def rollout(self, t0, T, obs=True):
+    def rollout(self, t0, T, obs=True, stats=False):
         def one(i):
             a, b = self.sl[i]
             acts = O.splitmix64_actions(ASEED, t0, T, b - a, offset=a)
-            return self.obs[i].rollout(acts, want_obs=obs, want_stats=False)
+            return self.obs[i].rollout(acts, want_obs=obs, want_stats=stats)
         rs = list(self.pool.map(one, range(len(self.sl))))
-        keys = ("reward", "done", "obs") if obs else ("reward", "done")
+        keys = ("reward", "done") + (("obs",) if obs else ()) + (("stats",) if stats else ())
         return {k: np.concatenate([r[k] for r in rs], axis=1) for k in keys}
 
     def final_state(self):

@@ -86,33 +86,59 @@ def test_two_ranks_gather_equals_one_batch(tmp_path):
     assert got["done"].any()  # auto-resets happened inside the compared span
 
 
-def test_bench_gpus2_direct_invocation():
-    env = dict(os.environ, ST_BENCH_SHARED_GPU="1")
+def check_bench_dump(path, n_global, steps):
+    """bench.py's C5 region (ST_BENCH_DUMP): rank 0's assembled outputs of the
+    last timed step -- gathered from every rank -- against the oracle stepping
+    all n_global envs through the same `steps` action rows (seeds 1000 + e,
+    the bench's splitmix64 actions keyed by the global index)."""
+    from test_gpu_long_horizon import ParallelOracle
+    z = np.load(path)
+    assert int(z["n_global"]) == n_global and int(z["step"]) == steps - 1
+    orc = ParallelOracle(n_global, {})
+    try:
+        if steps > 1:
+            orc.rollout(0, steps - 1, obs=False)
+        ref = orc.rollout(steps - 1, 1)
+    finally:
+        orc.close()
+    assert np.array_equal(z["reward"], ref["reward"][0])
+    assert np.array_equal(z["done"].astype(np.uint8), ref["done"][0])
+    assert np.array_equal(z["obs"].T, ref["obs"][0])
+    return z
+
+
+def test_bench_gpus2_direct_invocation(tmp_path):
+    env = dict(os.environ, ST_BENCH_SHARED_GPU="1", ST_BENCH_DUMP=str(tmp_path / "c5.npz"))
     env.pop("WORLD_SIZE", None)
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
                         "--steps", "30", "--warmup", "5", "--n-envs", "8192", "--no-cpu-baseline",
-                        "--no-clear-heavy", "--gather-steps", "20"],
+                        "--no-clear-heavy"],
                        env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1  # rank 0 prints one JSON line
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["envs_total"] == 2 * 8192
-    assert d["value"] > 0 and d["gather_variant"]["steps"] == 20
+    assert d["value"] > 0 and d["gather"]["gathers_in_timed_region"] == 30
+    assert d["step_no_gather"]["value"] > 0
     assert d["scaling"] == "weak"
+    z = check_bench_dump(tmp_path / "c5.npz", 2 * 8192, 35)
+    assert int(z["gathers_timed"]) == 30
 
 
-def test_bench_rccl_calls_one_rank():
+def test_bench_rccl_calls_one_rank(tmp_path):
     """The nccl (RCCL) side of bench.py on a one-GPU box: init with device_id,
     barriers, the MAX all-reduce of the timings and the double-buffered async
-    gather, at one rank (two ranks cannot share a GPU under RCCL)."""
+    gather of the C5 region, at one rank (two ranks cannot share a GPU under
+    RCCL); the gathered outputs of the last timed step equal the oracle's."""
     env = dict(os.environ, ST_BENCH_FORCE_DIST="1", RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
-               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), ST_BENCH_DUMP=str(tmp_path / "c5.npz"))
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--backend", "nccl",
                         "--steps", "30", "--warmup", "5", "--n-envs", "8192", "--no-cpu-baseline",
-                        "--no-clear-heavy", "--gather-steps", "20"],
+                        "--no-clear-heavy"],
                        env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, p.stderr[-2000:]
     d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
-    assert d["gather_variant"]["backend"] == "nccl" and d["gather_variant"]["steps"] == 20
+    assert d["gather"]["backend"] == "nccl" and d["gather"]["gathers_in_timed_region"] == 30
     assert d["value"] > 0
+    check_bench_dump(tmp_path / "c5.npz", 8192, 35)

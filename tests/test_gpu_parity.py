@@ -651,15 +651,17 @@ def test_async_action_check():
     with pytest.raises(KeyError):
         a.check_actions()
     # wider dtypes: values a uint8 cast would wrap into 0..6
-    for badv, dt in ((256, torch.int64), (-1, torch.int64), (263, torch.int32), (2.5, torch.float32)):
+    for badv, dt in ((256, torch.int64), (-1, torch.int64), (263, torch.int32), (2.5, torch.float32),
+                     (-1, torch.int8), (127, torch.int8), (-1, torch.int16), (256, torch.int16)):
         x = b.gen_actions(300, 3).to(dt)
         x[5] = badv
         a.step(x)
         with pytest.raises(KeyError):
             a.check_actions()
-    x = b.gen_actions(301, 3).to(torch.float64)  # integral floats are keys (2.0 == 2)
-    a.step(x)
-    a.check_actions()
+    for dt in (torch.float64, torch.int8, torch.int16):  # in-range values of every dtype pass (2.0 == 2)
+        x = b.gen_actions(301, 3).to(dt)
+        a.step(x)
+        a.check_actions()
     # the kernel on its own
     L = a._L
     sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
