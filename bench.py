@@ -389,7 +389,7 @@ def main():
     def kname_of(kind, f32, sc0, n=None):  # rocprofv3's demangled name of the 10x20 kernel
         b = lambda v: "true" if v else "false"  # noqa: E731
         if kind == "step":
-            return f"k_step<10, 20, {b(f32)}, false, {b(sc0)}>"
+            return f"k_step<10, 20, {b(f32)}, false, {b(sc0)}, false>"
         if rollout_three_wave(n):
             return f"k_rollout<10, 20, {b(f32)}, {b(sc0)}, false>"
         return f"k_rollout2<10, 20, {b(f32)}, {b(sc0)}>"

@@ -209,11 +209,11 @@ def test_bench_roofline_bytes_and_pmc_tie(tmp_path, monkeypatch):
     assert abs(bench.algorithmic_bytes(10, 20, 1.0, False) - (102 + 167.7)) < 1e-9
     assert bench.step_grid(4096) == 8192 and bench.step_grid(65536) == 131072
     assert len(bench.kernel_source_sha()) == 16
-    step = bench.launch_key("k_step<10, 20, false, false, true>", bench.step_grid(65536), 1)
+    step = bench.launch_key("k_step<10, 20, false, false, true, false>", bench.step_grid(65536), 1)
     ro = bench.launch_key("k_rollout<10, 20, false, true>", bench.step_grid(65536), 100)
     assert step.endswith("@131072@k1") and ro.endswith("@131072@k100")
     assert pmc_summary.launch_k("void st::(anonymous namespace)::k_rollout<10, 20, false, true>(st::KParams)", 100) == 100
-    assert pmc_summary.launch_k("void st::(anonymous namespace)::k_step<10, 20, false, false, true>(st::KParams)", 100) == 1
+    assert pmc_summary.launch_k("void st::(anonymous namespace)::k_step<10, 20, false, false, true, false>(st::KParams)", 100) == 1
     sha = bench.kernel_source_sha()
     prof = tmp_path / "profiles"
     prof.mkdir()
@@ -255,7 +255,7 @@ def test_committed_profiles_match_sources():
     trs = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_trace.json")))
     d, tj = json.load(open(pmcs[-1])), json.load(open(trs[-1]))
     assert d["kernel_source_sha"] == tj["kernel_source_sha"] == bench.kernel_source_sha()
-    head = bench.launch_key("k_step<10, 20, false, false, true>", bench.step_grid(65536), 1)
+    head = bench.launch_key("k_step<10, 20, false, false, true, false>", bench.step_grid(65536), 1)
     assert head in d["kernels"] and head in tj["kernels"]
     assert tj["kernels"][head]["p_lock"] is not None
 

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-3 GPU check + bench lines: the -m gpu suite, smoke, the default
+# GPU check + bench lines (TAG=r04 bash tools/gpu_final.sh): the -m gpu suite, smoke, the default
 # bench (K = 4,000) and the driver's shape (K = 20).
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"; export TMPDIR=/tmp
-mkdir -p gpurun_out; TAG=${TAG:-r03}
+mkdir -p gpurun_out; TAG=${TAG:-r04}
 timeout -k 10 1000 python -u -m pytest tests -x -v -m gpu --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 \
  && echo "pytest ok" \
  && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 \
