@@ -270,6 +270,9 @@ def main():
                          "(measured: graph replay 2.5%% slower at K=4000, noisier at K=20; "
                          "profiles/r02_launch_ab.jsonl)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    ap.add_argument("--gather-format", choices=("wire", "rows"), default="wire",
+                    help="C5 (--gpus > 1, packed obs): what each step gathers to rank 0 -- st_step_wire's "
+                         "bit stream (28 B per 10x20 env) or st_step's obs/reward/done rows (48 B)")
     ap.add_argument("--rollout-chunk", type=int, default=100, help="steps per st_rollout launch")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -490,17 +493,28 @@ def main():
 
         # ---- BASELINE C5: every step's outputs gathered to rank 0 ----
         def setup_gather(self):
-            """Two [W+2][n] output buffers (packed obs | reward | done, the
-            layout distributed.gather_outputs sends), rank 0's receive lists,
-            and the ctypes arguments of every step writing into buffer t % 2."""
+            """Two output buffers -- st_step_wire's [words][n] rows (the
+            default with packed obs) or st_step's [W+2][n] packed obs | reward
+            | done (distributed.output_buffer) -- rank 0's receive lists, and
+            the ctypes arguments of every step writing into buffer t % 2."""
             self.nccl = args.backend == "nccl"
-            self.gbufs = [output_buffer(W, self.n_local, dev) for _ in range(2)]
-            views = [[ctypes.c_void_p(v.data_ptr()) for v in buffer_views(b, W)] for b in self.gbufs]
+            self.wire = args.gather_format == "wire" and not self.f32
+            if self.wire:
+                self.gbufs = [torch.zeros((self.eng.wire_words, self.n_local), dtype=torch.int32, device=dev)
+                              for _ in range(2)]
+                self.gfn = self.eng._L.st_step_wire
+            else:
+                self.gbufs = [output_buffer(W, self.n_local, dev) for _ in range(2)]
+                self.gfn = self.fn
+                views = [[ctypes.c_void_p(v.data_ptr()) for v in buffer_views(b, W)] for b in self.gbufs]
             rdev = dev if self.nccl else torch.device("cpu")  # gloo gathers host tensors
             self.grecv = [[torch.empty(b.shape, dtype=b.dtype, device=rdev) for _ in range(world)]
                           if rank == 0 else None for b in self.gbufs]
             ctx = self.eng._ctx
-            if self.f32:
+            if self.wire:
+                self.gargs = [(ctx, self.aptr[t], ctypes.c_void_p(self.gbufs[t & 1].data_ptr()), sp)
+                              for t in range(WU + K)]
+            elif self.f32:
                 self.gargs = [(ctx, self.aptr[t], views[t & 1][0], self.pf, views[t & 1][1], views[t & 1][2], sp)
                               for t in range(WU + K)]
             else:
@@ -515,7 +529,7 @@ def main():
             it behind the current stream, s), so step t+1 overlaps the gather
             of step t; before step t+2 reuses a buffer, s waits for the gather
             that read it.  All gathers are complete on s when this returns."""
-            fn, rc = self.fn, 0
+            fn, rc = self.gfn, 0
             for t in range(t0, t1):
                 k = t & 1
                 if self.gworks[k] is not None:
@@ -548,8 +562,12 @@ def main():
             dump = os.environ.get("ST_BENCH_DUMP")
             if rank == 0 and dump:
                 import numpy as np
-                from gym_simpletetris_amd.distributed import assemble
-                o, r, d = assemble([b.cpu() for b in self.grecv[(WU + K - 1) & 1]], W)
+                from gym_simpletetris_amd.distributed import assemble, assemble_wire
+                got = self.grecv[(WU + K - 1) & 1]
+                if self.wire:  # rank 0 unpacks the gathered rows (st_unwire), outside the region
+                    o, r, d = (x.cpu() for x in assemble_wire(got, W, H))
+                else:
+                    o, r, d = assemble([b.cpu() for b in got], W)
                 np.savez(dump, obs=o.numpy().view(np.uint32), reward=r.numpy(), done=d.numpy(),
                          step=WU + K - 1, n_global=self.n_global, gathers_timed=ng)
             bpr = self.gbufs[0].numel() * 4
@@ -557,6 +575,9 @@ def main():
             return {"value": self.n_global * K / el, "ms_per_step": ms, "event_ms_per_step": ev_ms / K,
                     "p_lock": p_lock, "gathers_timed": ng,
                     "gather": {"backend": args.backend, "collective": "torch.distributed.gather to rank 0",
+                               "format": ("st_step_wire: %d words per env (obs bits, reward low 16, done)"
+                                          % self.eng.wire_words if self.wire else
+                                          "st_step rows: packed obs [W] + reward + done per env"),
                                "gathers_in_timed_region": ng, "bytes_per_rank_per_step": bpr,
                                "bytes_into_rank0_per_step": bpr * (world - 1),
                                "rank0_ingress_GBps": bpr * (world - 1) / (ms * 1e-3) / 1e9,
@@ -641,7 +662,8 @@ def main():
         "data": "synthetic (uniform splitmix64 actions, seeds 1000 + global env index)",
         "config": {
             "workload": (f"C5: {head.n_global} boards sharded {args.n_envs} per GPU x {world}, one st_step per "
-                         f"shard per step + a gather of its packed obs/reward/done to rank 0 per step, "
+                         f"shard per step + a gather of its obs/reward/done to rank 0 per step "
+                         f"({'st_step_wire bit stream' if args.gather_format == 'wire' and not f32 else 'rows'}), "
                          if use_dist else
                          f"{args.config.upper()}: {args.n_envs} parallel {W}x{H} boards per GPU, one "
                          f"st_step per step, ")

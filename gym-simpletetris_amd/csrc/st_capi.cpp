@@ -223,6 +223,34 @@ int st_step_vec(st_ctx *c, const uint8_t *d_actions, uint32_t *d_obs, float *d_o
     return step_impl(c, d_actions, d_obs, d_obs_f32, d_reward, d_done, stream, d_final_obs, d_info);
 }
 
+int st_wire_words(int32_t width, int32_t height) {
+    if (width < 1 || height < 1 || width > st::kMaxW || height > st::kMaxH)
+        return fail(ST_EINVAL, "st_wire_words: board %dx%d outside 1..%d x 1..%d", width, height, st::kMaxW,
+                    st::kMaxH);
+    return (width * height + 17 + 31) / 32;
+}
+
+int st_step_wire(st_ctx *c, const uint8_t *d_actions, uint32_t *d_wire, st_stream stream) {
+    if (!c || !d_actions || !d_wire) return fail(ST_EINVAL, "st_step_wire: null argument");
+    if (!c->seeded || !c->reset_once)
+        return fail(ST_ESTATE, "st_step_wire before st_seed + st_reset (tetris_env.py:244 needs an anchor)");
+    DeviceGuard g(c->device);
+    st::KParams p = params(c);
+    p.actions = d_actions;
+    p.wire = d_wire;
+    ST_HIP(st::launch_step(p, (hipStream_t)stream));
+    return ST_OK;
+}
+
+int st_unwire(int32_t width, int32_t height, int64_t n, const uint32_t *d_wire, uint32_t *d_obs,
+              int32_t *d_reward, uint8_t *d_done, st_stream stream) {
+    if (st_wire_words(width, height) < 0) return ST_EINVAL;
+    if (n < 0) return fail(ST_EINVAL, "st_unwire: negative size");
+    if (n > 0 && (!d_wire || !d_obs || !d_reward || !d_done)) return fail(ST_EINVAL, "st_unwire: null argument");
+    ST_HIP(st::launch_unwire(width, height, n, d_wire, d_obs, d_reward, d_done, (hipStream_t)stream));
+    return ST_OK;
+}
+
 int st_rollout(st_ctx *c, int32_t k, const uint8_t *d_actions, uint32_t *d_obs, float *d_obs_f32,
                int32_t *d_reward, uint8_t *d_done, st_stream stream) {
     if (!c || !d_actions) return fail(ST_EINVAL, "st_rollout: null argument");

@@ -35,7 +35,8 @@ struct KParams {
     uint32_t ablate;    // TIMING DIAGNOSTICS ONLY (env ST_ABLATE at st_create, read only by
                         // -DST_ABLATION=1 builds, tools/ablate.sh); 0 in
                         // every correct run: 1 = no lock path, 2 = no MT draw,
-                        // 4 = no twist, 8 = no obs output
+                        // 4 = no twist, 8 = no obs output; st_step: 1024 =
+                        // counter rows read from the first workgroup's lines
     uint64_t *stamps;   // DIAGNOSTIC build only (env ST_STAMPS at st_create): per-wave
                         // s_memtime at 8 phase boundaries of the step kernel
     int32_t k;          // st_rollout: number of steps
@@ -56,6 +57,7 @@ struct KParams {
     uint8_t *done;           // [n]
     uint32_t *act_flag;      // st_set_action_flag: sticky "action outside 0..6" word, or null
     uint32_t *final_obs;     // st_step_vec: [W][n] terminal obs of envs reset in the step, or null
+    uint32_t *wire;          // st_step_wire: [st_wire_words(W, H)][n] gather format, or null
     int32_t *info;           // st_step_vec: [ST_NSTAT][n] counters after the step, or null
     int32_t cus;             // compute units of the device (launch_rollout's kernel choice)
 };
@@ -73,6 +75,8 @@ hipError_t launch_policy_greedy(const KParams &p, uint64_t seed, int64_t t, uint
                                 uint8_t *out, hipStream_t s);
 hipError_t launch_grayscale(const KParams &p, const uint32_t *obs, int size, int channels,
                             int as_u8, void *out, hipStream_t s);
+hipError_t launch_unwire(int W, int H, int64_t n, const uint32_t *wire, uint32_t *obs, int32_t *reward,
+                         uint8_t *done, hipStream_t s);
 hipError_t launch_check_actions(const uint8_t *a, int64_t n, uint32_t *flag, hipStream_t s);
 hipError_t launch_gen_actions(uint8_t *out, int64_t n, int64_t t, uint64_t seed, int64_t off,
                               hipStream_t s);

@@ -127,28 +127,22 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uin
 // `nt` stores stream out during the kernel instead (A/B, st_step packed:
 // 6.31 -> 5.89 us with obs, board, counter and MT stores all `nt`).
 constexpr int kNT = 2;
-// A/B knob: issue priority of the draw wave after B1 (its chain is the
-// critical one there: st_step -1.5%, rollouts -6% at 2)
-#ifndef ST_DPRIO
-#define ST_DPRIO 2
+// Wave issue priorities (s_setprio), settled by A/B in rounds 1-3:
+// the draw wave after B1 at 2 (its chain was the critical one there: st_step
+// -1.5%, rollouts -6%; 0 / 1 / 3 re-checked in round 3 within noise,
+// profiles/r03/ab_step_prio.txt); st_step's logic wave at 1 from its first
+// instruction (since the draw parameters moved before B1 its chain is the
+// step: K = 2,000 4.67-4.72 -> 4.64-4.67 us, profiles/r03/ab_step_lprio.txt).
+constexpr int kDrawPrio = 2;
+// st_step's late counters (see run_steps, LCL / LCD): bit 0 the logic
+// wave's lock-path rows (adopted: K = 2,000 4.642-4.643 -> 4.605-4.635 us,
+// steady 4.533-4.539 -> 4.494-4.516), bit 1 the draw wave's shape counts
+// (+6%: its post-B1 chain, window + counts + draw parameters, becomes the
+// step's); profiles/r04/ab_late_counters.txt
+#ifndef ST_LC
+#define ST_LC 1
 #endif
-#ifndef ST_LPRIO
-#define ST_LPRIO 0
-#endif
-// st_step's logic wave at issue priority 1 from its first instruction: since
-// the draw wave's parameters moved before B1 the logic wave's chain is the
-// step (A/B, 3 alternating rounds, K = 2,000: 4.67-4.72 -> 4.64-4.67 us,
-// steady burst 4.74-4.75 -> 4.68-4.71; profiles/r03/ab_step_lprio.txt)
-#ifndef ST_LPRIO0
-#define ST_LPRIO0 1
-#endif
-// st_step: the obs overlay goes to a plane of its own (OV), so the board and
-// obs rows are read in ONE transposed pass and stored together (A/B, 2 rounds
-// on one box, K = 2,000: 4.82-4.84 -> 4.80-4.81 us; tools/ab_step_libs.sh,
-// profiles/r03/ab_step_k1.txt)
-#ifndef ST_OVPLANE
-#define ST_OVPLANE 1
-#endif
+constexpr int kLogicPrio = 1;
 template <int AUX = 0>
 __device__ __forceinline__ void buf_store16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
     const i32x4 d = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
@@ -794,18 +788,15 @@ struct StepLds {
     uint32_t SS[kHotQ * 4 * kWave] __attribute__((aligned(16)));
     uint32_t T2[2 * 28] __attribute__((aligned(8)));  // piece table {m, g}
     uint32_t S[kMtN];                                  // mt_finish scratch
-    // st_step: per env board keep-mask, changed board columns, changed
-    // counter rows of the logic (SD) and draw (SDD) waves
+    // st_step: per env board keep-mask, changed board columns
     uint32_t KM[KSTEPS == 1 ? kWave : 4] __attribute__((aligned(16)));
     uint32_t BD[KSTEPS == 1 ? kWave : 4] __attribute__((aligned(16)));
-    uint32_t SD[KSTEPS == 1 ? kWave : 4] __attribute__((aligned(16)));
-    uint32_t SDD[KSTEPS == 1 ? kWave : 4] __attribute__((aligned(16)));
     // float32 obs writer (F32): per-lane obs words at stride W+1 (conflict-
     // free transposed reads) and the 16 float4 patterns of a 4-bit nibble
     uint32_t O[F32 ? kWave * (kMaxW + 1) : 1];
     float F4[F32 ? 64 : 4] __attribute__((aligned(16)));
-    // st_step (ST_OVPLANE): the obs overlay plane, laid out like L
-    uint32_t OV[KSTEPS == 1 && ST_OVPLANE ? kCols * kWave : 4] __attribute__((aligned(16)));
+    // st_step: the obs overlay plane, laid out like L
+    uint32_t OV[KSTEPS == 1 ? kCols * kWave : 4] __attribute__((aligned(16)));
     // two-wave st_step hand-offs (see run_steps)
     uint32_t dump[kWave] __attribute__((aligned(16)));  // the logic wave's padding-row writes
     // (step-parity double buffers where a wave may write step t+1's value
@@ -826,8 +817,7 @@ struct StepLds {
 // (every spawn / reset still consumes the next draw, with the shape counts of
 // that moment: the preview is drawn right after the previous spawn's count
 // update, and counts change only at spawns); st_mt_sync rewinds the preview's
-// words for the host.  Rollouts run both roles in one wave (kRoleOne).
-constexpr int kRoleOne = 0;
+// words for the host.  k_rollout2 (KSTEPS == 0) runs the same two roles.
 constexpr int kRoleL = 1;
 constexpr int kRoleD = 2;
 
@@ -836,20 +826,42 @@ __device__ __forceinline__ void wg_barrier() {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
-// One-way LDS hand-off between the two waves of a workgroup without a
-// barrier (the writer must not wait for the reader).  A wave's LDS accesses
-// execute in order, so data it wrote before the flag are visible to a wave
-// that has seen the flag; the asm statements only keep the compiler from
-// moving LDS accesses across the hand-off (no s_waitcnt: the writer's
-// outstanding global stores are not drained).
+// One-way LDS hand-off between the waves of a workgroup without a barrier
+// (the writer must not wait for the reader).
+//
+// Ordering.  The flag is a workgroup-scope atomic; the writer's release fence
+// and the reader's acquire fence are restricted to the LDS address space
+// (the "local" memory-model-relaxation annotation of __builtin_amdgcn_fence):
+// on gfx950 they lower to `s_waitcnt lgkmcnt(0)` only.  An unrestricted
+// workgroup-scope fence would also wait `vmcnt(0)` -- every outstanding
+// global load and store of the wave, e.g. the draw wave's MT window -- which
+// is what a volatile access or an asm memory clobber here cost in round 1.
+// With the fences, the data a writer stores before lds_flag_set happen-before
+// the reader's accesses after lds_flag_wait in the C++ / HIP model, and no
+// plain access races.
+//
+// Where a reader takes the flag AND the data it guards in one LDS round trip
+// (the rollout's queue / action ring and consumption mask: the flag is read,
+// the data are read right behind it, and the flag is checked after both
+// return), the data are read as relaxed workgroup-scope atomics (lds_ld; the
+// writers store them with lds_st), so there is no data race, and the order
+// of the two reads rests on the hardware: the LLVM AMDGPU memory model
+// (AMDGPUUsage, "Memory Model GFX942", which gfx950 follows) states that the
+// LDS operations of a wavefront are executed in order, so no fence is needed
+// between LDS accesses of one wavefront and `s_waitcnt lgkmcnt` only waits
+// for their results.  The signal fences keep the compiler from reordering
+// the two reads (they emit nothing).
 // (LDS address space explicitly: through a generic pointer the accesses
 // become flat_* instructions, which count in vmcnt and wait for it.)
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
-// (Relaxed atomics + compiler-only fences: a volatile access or an asm memory
-// clobber here makes the compiler wait for every outstanding load first --
-// vmcnt(0) -- which cost the draw wave its whole MT-window latency.)
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t *p) {
+    return __hip_atomic_load((const lds_u32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v) {
+    __hip_atomic_store((lds_u32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 __device__ __forceinline__ void lds_flag_set(uint32_t *f, uint32_t v) {
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __hip_atomic_store((lds_u32 *)f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
@@ -857,7 +869,7 @@ __device__ __forceinline__ void lds_flag_wait(uint32_t *f, uint32_t v) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     while (__hip_atomic_load((lds_u32 *)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != v)
         __builtin_amdgcn_s_sleep(1);
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 // A progress counter read as a relaxed LDS atomic (no wait by itself).
 __device__ __forceinline__ uint32_t lds_flag_get(uint32_t *f) {
@@ -868,19 +880,20 @@ __device__ __forceinline__ void lds_flag_wait_ge(uint32_t *f, uint32_t v) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     while ((int32_t)(__hip_atomic_load((lds_u32 *)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) - v) < 0)
         __builtin_amdgcn_s_sleep(1);
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// KSTEPS == 1: TetrisEngine.step once (st_step), ROLE = kRoleL / kRoleD (the
-// two waves of a workgroup) or kRoleOne; KSTEPS == 0: p.k consecutive steps
-// (st_rollout, kRoleOne) with the board and counters kept in LDS between
-// steps, actions read one step ahead, and per-step outputs at [t].  State is
+// ROLE = kRoleL / kRoleD: the logic or the draw wave of a workgroup.
+// KSTEPS == 1: TetrisEngine.step once (st_step); KSTEPS == 0: p.k consecutive
+// steps (k_rollout2, st_rollout above 4 workgroups per CU) with the board and
+// counters kept in LDS between steps, actions read one step ahead, and
+// per-step outputs at [t].  State is
 // loaded once at the start and stored once at the end.
 // SC0: the context has no scoring flags (the reference's defaults,
 // tetris_env.py:126-137): those tests fold away at compile time (measured:
 // the rollout loop otherwise holds each flag as a 64-bit lane mask at the
 // SGPR limit, -5% packed rollout; st_step -1%).
-// VEC (st_step_vec, two-wave st_step only): the vector env's outputs -- with
+// VEC (st_step_vec): the vector env's outputs -- with
 // p.final_obs, an env reset in this step returns the reset obs (the empty
 // board clear() returns, tetris_env.py:306-315, :405-411) and its terminal
 // obs goes to final_obs; with p.info, every counter row after the step is
@@ -888,10 +901,10 @@ __device__ __forceinline__ void lds_flag_wait_ge(uint32_t *f, uint32_t v) {
 // the env was reset, else 0).
 template <int WT, int HT, bool F32, bool STAMP, int KSTEPS, bool SC0, int ROLE, bool VEC = false>
 __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KSTEPS> &sm) {
-    static_assert(!VEC || (KSTEPS == 1 && ROLE != kRoleOne), "VEC: the two-wave st_step only");
-    constexpr bool DO_L = ROLE != kRoleD;  // action, lock path, outputs
-    constexpr bool DO_D = ROLE != kRoleL;  // MT words, next-generation block, draws
-    constexpr bool TWO = ROLE != kRoleOne;
+    static_assert(ROLE == kRoleL || ROLE == kRoleD, "run_steps: the logic or the draw wave");
+    static_assert(!VEC || KSTEPS == 1, "VEC: st_step only");
+    constexpr bool DO_L = ROLE == kRoleL;  // action, lock path, outputs
+    constexpr bool DO_D = ROLE == kRoleD;  // MT words, next-generation block, draws
     [[maybe_unused]] uint64_t tstamp[12] = {};
     [[maybe_unused]] uint32_t tacc[12] = {};  // rollout stamp build: per-phase cycle totals
     [[maybe_unused]] uint64_t tlast = 0;
@@ -913,7 +926,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         tlast = __builtin_amdgcn_s_memtime();
     }
     ST_STAMP(0);
-    if constexpr (ROLE == kRoleL && KSTEPS == 1 && ST_LPRIO0 > 0) __builtin_amdgcn_s_setprio(ST_LPRIO0);
+    if constexpr (ROLE == kRoleL && KSTEPS == 1) __builtin_amdgcn_s_setprio(kLogicPrio);
     uint32_t *const L = sm.L;
     uint32_t *const SS = sm.SS;
     const int W = WT ? WT : p.W;
@@ -937,9 +950,27 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     const uint32_t loff = (uint32_t)(lane >> 4) * (uint32_t)sd + 4u * (uint32_t)(lane & 15);
     constexpr int NBQ = ((WT ? WT : kMaxW) + 3) / 4;  // board 4-row groups
     const uint32_t *bsrc = p.board + e0;
-    const uint32_t *ssrc = reinterpret_cast<const uint32_t *>(p.stats) + e0;
-    constexpr bool OVP = KSTEPS == 1 && ROLE != kRoleOne && ST_OVPLANE;
-    auto mine_q = [&](int q) { return ROLE == kRoleOne || (ROLE == kRoleL) == (q < 2); };
+    // (ablation 1024: every wave's counter groups from the first workgroup's
+    // lines -- the counter rows' HBM reads gone, timing only)
+    const uint32_t *ssrc = reinterpret_cast<const uint32_t *>(p.stats) + ((kAblate & 1024u) ? 0 : e0);
+    constexpr bool OVP = KSTEPS == 1;
+    // st_step (not st_step_vec, whose info snapshot needs every counter of
+    // every env): LATE COUNTERS.  The prologue's load burst carries only what
+    // every env needs at the step start -- board, action, time, piece word,
+    // MT word -- and the lock-only counter rows are read per locking lane
+    // once the lock decision is known (logic: score .. deaths, issued before
+    // B1, needed at the end of the lock path; draw: the shape counts, issued
+    // with the MT window after B1)
+    // (ST_LC: A/B knob, bit 0 the logic wave's rows, bit 1 the draw wave's)
+    constexpr bool LCL = KSTEPS == 1 && !VEC && (ST_LC & 1);
+    constexpr bool LCD = KSTEPS == 1 && !VEC && (ST_LC & 2);
+    // staged counter groups (rows 4q .. 4q + 3): logic 0-1, draw 2-3; with
+    // late rows only what the other role still reads early
+    auto mine_q = [&](int q) {
+        if constexpr (LCD) return !LCL && ROLE == kRoleL && q < 2;
+        if constexpr (LCL) return ROLE == kRoleD && q >= 1;
+        return (ROLE == kRoleL) == (q < 2);
+    };
     // Rows past the last real row (board padding, counter row 15) re-read the
     // last row -- the same cache line another lane fetches -- instead of
     // fetching padding; the loads stay unconditional (a load under a branch
@@ -967,7 +998,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     // (the draw wave's chain is the longer one).  (Measured and dropped: the
     // draw wave running the action phase itself instead of waiting at B1 --
     // the two concurrent action phases slowed the logic wave's by ~50%.)
-    constexpr bool STEP2 = TWO && KSTEPS == 1;
+    constexpr bool STEP2 = KSTEPS == 1;
     constexpr bool ACT = DO_L;
     // unconditional (clamped) so it is issued with the others; masked at use
     uint32_t act_next = 0;
@@ -982,12 +1013,14 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         pw_d = p.piece[e];
         tm_d = reinterpret_cast<const uint32_t *>(p.stats)[(int64_t)ST_STAT_TIME * sd + e];
     }
+    [[maybe_unused]] uint32_t mt_d = 0;  // LCD: the MT word per lane (both waves)
+    if constexpr (LCD) mt_d = reinterpret_cast<const uint32_t *>(p.stats)[(int64_t)ST_STAT_MT_INDEX * sd + e];
     // The piece table, lane i = entry i, from immediates (under the load
     // latency; no memory access: a __constant__ load gets sunk by the
     // compiler past the state loads' completion -- one more serialized round
     // trip).  Two waves: the draw wave builds it (and the walls, and the f32
     // nibble table).
-    constexpr bool BUILD = ROLE != kRoleL;
+    constexpr bool BUILD = DO_D;
     uint32_t tab_m = 0, tab_g = 0;
     if constexpr (BUILD) {
         // one v_writelane per entry (the constant in an SGPR: SALU): 56 VALU
@@ -1048,13 +1081,9 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             if ((WT || 4 * q < W) && 4 * q + lrow < W)
                 *reinterpret_cast<uint4 *>(&sm.OV[(4 * q + lrow + kPad) * kWave + lcc]) = make_uint4(0u, 0u, 0u, 0u);
     }
-    if constexpr (TWO) {
-        if (ROLE == kRoleL && lane == 0) sm.f1 = 0u;
-        if (ROLE == kRoleD && lane == 0) sm.f2 = 0u;
-        wg_barrier();  // B0: the staged state is complete
-    } else {
-        wave_sync();
-    }
+    if (ROLE == kRoleL && lane == 0) sm.f1 = 0u;
+    if (ROLE == kRoleD && lane == 0) sm.f2 = 0u;
+    wg_barrier();  // B0: the staged state is complete
     auto ss = [&](int r) -> uint32_t & { return SS[r * kWave + lane]; };
     auto tab = [&](int i) -> uint2 { return *reinterpret_cast<const uint2 *>(&sm.T2[2 * i]); };
     // an action outside value_action_map in any step of this launch (the
@@ -1079,7 +1108,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     // MT word at the start of the step (the logic wave uses only the preview
     // bits; in a two-wave step the draw wave replaces the row after B1, and in
     // a two-wave rollout it hands step t-1's word over in mtw: read after B1)
-    uint32_t mt0 = ss(ST_STAT_MT_INDEX);
+    uint32_t mt0 = LCD ? mt_d : ss(ST_STAT_MT_INDEX);
     if constexpr (STAMP && KSTEPS == 1) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     ST_STAMP(1);
 
@@ -1134,6 +1163,17 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         }
     }
     ST_STAMP(2);
+    // LC: the logic wave's lock-path counters, per locking lane (an
+    // out-of-range offset elsewhere: no traffic, 0)
+    [[maybe_unused]] uint32_t lcv[5] = {};
+    if constexpr (LCL && DO_L) {
+        const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
+        const uint32_t eo = (uint32_t)e * 4u;
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+            lcv[j] = __builtin_amdgcn_raw_buffer_load_b32(
+                rs, locknow ? eo + (uint32_t)(ST_STAT_SCORE + j) * (uint32_t)sd * 4u : kOff, 0, 0);
+    }
     // the draw wave's next-generation chunk of this step: operands issued
     // before B1, so they arrive while it waits for the lock decision
     [[maybe_unused]] MtChunk chunk;
@@ -1148,33 +1188,32 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     if constexpr (DO_D) {
         mrs = mt_res(p.mt + e0 * kMtPitch, lane);
         mt_chunk_issue(mrs, mt0, real && !(kAblate & 2u), lane, chunk);
-        const int s0 = pv_id(mt0);
+        if constexpr (!LCD) {
+            const int s0 = pv_id(mt0);
 #pragma unroll
-        for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)ss(ST_STAT_COUNT0 + i) + (i == s0);  // _new_piece :199
-        csid = cnt[0];
+            for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)ss(ST_STAT_COUNT0 + i) + (i == s0);  // _new_piece :199
+            csid = cnt[0];
 #pragma unroll
-        for (int i = 1; i < 7; ++i) csid = s0 == i ? cnt[i] : csid;
-        dpar = draw_par(cnt);
+            for (int i = 1; i < 7; ++i) csid = s0 == i ? cnt[i] : csid;
+            dpar = draw_par(cnt);
+        }
     }
-    if constexpr (TWO) {
-        if constexpr (DO_L) {
-            const uint64_t m = __ballot(locknow);
-            if (lane == 0) {
-                sm.lockm[t & 1][0] = (uint32_t)m;
-                sm.lockm[t & 1][1] = (uint32_t)(m >> 32);
-            }
+    if constexpr (DO_L) {
+        const uint64_t m = __ballot(locknow);
+        if (lane == 0) {
+            sm.lockm[t & 1][0] = (uint32_t)m;
+            sm.lockm[t & 1][1] = (uint32_t)(m >> 32);
         }
-        wg_barrier();  // B1: the draw wave learns which lanes lock
-        if constexpr (DO_D || KSTEPS != 1) ST_STAMP(10);
-        if constexpr (DO_D && ST_DPRIO > 0) __builtin_amdgcn_s_setprio(ST_DPRIO);
-        if constexpr (DO_L && ST_LPRIO > 0) __builtin_amdgcn_s_setprio(ST_LPRIO);
-        if constexpr (DO_D) {
-            const uint32_t w = lane < 32 ? sm.lockm[t & 1][0] : sm.lockm[t & 1][1];
-            locknow = (w >> (lane & 31)) & 1u;
-        }
-        if constexpr (DO_L && KSTEPS != 1) {
-            if (t > 0) mt0 = sm.mtw[(t - 1) & 1][lane];
-        }
+    }
+    wg_barrier();  // B1: the draw wave learns which lanes lock
+    if constexpr (DO_D || KSTEPS != 1) ST_STAMP(10);
+    if constexpr (DO_D) __builtin_amdgcn_s_setprio(kDrawPrio);
+    if constexpr (DO_D) {
+        const uint32_t w = lane < 32 ? sm.lockm[t & 1][0] : sm.lockm[t & 1][1];
+        locknow = (w >> (lane & 31)) & 1u;
+    }
+    if constexpr (DO_L && KSTEPS != 1) {
+        if (t > 0) mt0 = sm.mtw[(t - 1) & 1][lane];
     }
 
     // ---------------- draw: MT window, issued now ----------------
@@ -1186,18 +1225,35 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     constexpr int kWin = STEP2 ? 8 : 16;
     MtPre pre;
     if constexpr (DO_D) mt_pre_load<kWin>(mrs, mtst, want_pre, pre);
+    // LC: the shape counts of the locking lanes, with the window
+    [[maybe_unused]] uint32_t lcc7[7] = {};
+    if constexpr (LCD && DO_D) {
+        const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
+        const uint32_t eo = (uint32_t)e * 4u;
+#pragma unroll
+        for (int i = 0; i < 7; ++i)
+            lcc7[i] = __builtin_amdgcn_raw_buffer_load_b32(
+                rs, locknow ? eo + (uint32_t)(ST_STAT_COUNT0 + i) * (uint32_t)sd * 4u : kOff, 0, 0);
+    }
 
     // ---------------- logic: lock path (tetris_env.py:263-299) ----------------
     bool died = false, spawn = false;
     int32_t score = 0, lines = 0, holes = 0, height = 0, deaths = 0;
     int32_t o_score = 0, o_lines = 0, o_holes = 0, o_height = 0, o_deaths = 0;  // (dirty tests)
+    [[maybe_unused]] bool hset = false;  // LC: height set by the lock path
     uint32_t bdirty = 0;  // st_step: board columns this step changes (stores skip the rest)
     if (DO_L && locknow) {
-        score = o_score = (int32_t)ss(ST_STAT_SCORE);
-        lines = o_lines = (int32_t)ss(ST_STAT_LINES);
-        holes = o_holes = (int32_t)ss(ST_STAT_HOLES);
-        height = o_height = (int32_t)ss(ST_STAT_PIECE_HEIGHT);
-        deaths = o_deaths = (int32_t)ss(ST_STAT_DEATHS);
+        // (LC: score / lines / deaths count from 0 here -- deltas, added to
+        // the late-loaded values where they are stored, long after the lock
+        // path; the old holes / height are read only by the scoring flags
+        // that need them)
+        if constexpr (!LCL) {
+            score = o_score = (int32_t)ss(ST_STAT_SCORE);
+            lines = o_lines = (int32_t)ss(ST_STAT_LINES);
+            holes = o_holes = (int32_t)ss(ST_STAT_HOLES);
+            height = o_height = (int32_t)ss(ST_STAT_PIECE_HEIGHT);
+            deaths = o_deaths = (int32_t)ss(ST_STAT_DEATHS);
+        }
         paint<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
         // Column words carry the floor bits, so the topmost cell of column v
         // is ctz(v) (H when empty) and its holes are H - ctz(v) - popc(v & hmask):
@@ -1280,17 +1336,19 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             died = true;
             rew = -100;
         } else {  // :283-299
-            const int32_t old_holes = holes;
+            const int32_t old_holes = LCL ? 0 : holes;
             holes = nh;
             const int32_t hgt = __builtin_popcount(orv);  // sum(np.any(board, axis=0))
             if (kFlags & ST_PENALISE_HEIGHT) {
                 rew -= hgt;
             } else if (kFlags & ST_PENALISE_HEIGHT_INCREASE) {
-                if (hgt > height) rew -= 10 * (hgt - height);
+                const int32_t oh = LCL ? (int32_t)lcv[3] : height;
+                if (hgt > oh) rew -= 10 * (hgt - oh);
                 height = hgt;
+                hset = true;
             }
             if (kFlags & ST_PENALISE_HOLES) rew -= 5 * holes;
-            else if (kFlags & ST_PENALISE_HOLES_INCREASE) rew -= 5 * (holes - old_holes);
+            else if (kFlags & ST_PENALISE_HOLES_INCREASE) rew -= 5 * (holes - (LCL ? (int32_t)lcv[2] : old_holes));
             spawn = true;
         }
     }
@@ -1300,14 +1358,12 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     // a lock consumes the preview (spawn, or the same-step reset's new piece);
     // a death without auto-reset does not (the next st_reset takes it)
     bool draw = spawn || reset_now;
-    if constexpr (TWO) {
-        if (DO_L && p.autoreset != ST_AUTORESET_SAME_STEP) {
-            const uint64_t m = __ballot(draw);
-            if (lane == 0) {
-                sm.drawm[0] = (uint32_t)m;
-                sm.drawm[1] = (uint32_t)(m >> 32);
-                lds_flag_set(&sm.f1, (uint32_t)t + 1u);
-            }
+    if (DO_L && p.autoreset != ST_AUTORESET_SAME_STEP) {
+        const uint64_t m = __ballot(draw);
+        if (lane == 0) {
+            sm.drawm[0] = (uint32_t)m;
+            sm.drawm[1] = (uint32_t)(m >> 32);
+            lds_flag_set(&sm.f1, (uint32_t)t + 1u);
         }
     }
     uint2 odesc = desc;
@@ -1405,24 +1461,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 buf_store16<kNT>(rb, dirty ? boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff, v);
             }
         }
-        if constexpr (OVP) {
-            // (below: the ragged / unaligned obs path and the float32 writer
-            // read the planes per env; nothing is painted into L)
-        } else {
-        wave_sync();  // the board reads above precede the overlay paint
-        if constexpr (TWO) {
-            // the obs overlay of every lane at once: the current piece, or for
-            // a spawn the preview at the spawn position (known since the step
-            // started); a spawn without a preview gets its piece below, once
-            // the draw wave has drawn it
-            const uint2 pd = tab(pv_id(mt0) * 4);
-            const bool pvs = spawn && pv_ok(mt0);
-            paint<S32>(L, lane, pvs ? pd.x : desc.x, pvs ? pd.y : desc.y, pvs ? W / 2 : ax, pvs ? 0 : ay,
-                       spawn && !pvs ? 0u : hmask);
-        } else {
-            if (!spawn) paint<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
-        }
-        }  // !OVP
+        // (below: the ragged / unaligned obs path and the float32 writer read
+        // the planes per env; nothing is painted into L)
     }
 
     ST_STAMP(8);  // (stamp 8: between the early stores and the draw)
@@ -1432,13 +1472,22 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     if constexpr (DO_D) {
         // speculative in the draw wave (it does not know yet which locking
         // lanes die without auto-reset): committed below only where `draw`
-        const bool dr_spec = TWO ? locknow : draw;
+        const bool dr_spec = locknow;
         if constexpr (STAMP) {  // diagnostic split of the draw: MT-word wait | compute
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             ST_STAMP(9);
         }
         [[maybe_unused]] const uint32_t mt_before = mtst;
         uint32_t mt_new = mtst;
+        if constexpr (LCD) {
+            const int s0 = pv_id(mt0);
+#pragma unroll
+            for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)lcc7[i] + (i == s0);  // _new_piece :199
+            csid = cnt[0];
+#pragma unroll
+            for (int i = 1; i < 7; ++i) csid = s0 == i ? cnt[i] : csid;
+            dpar = draw_par(cnt);
+        }
         if (!(kAblate & 2u)) {
             mt_win_consume<kWin>(pre);
             const bool need1 = dr_spec && !pv_ok(mt0);
@@ -1446,7 +1495,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 // the piece first, with the counts before the spawn
                 int32_t c0[7];
 #pragma unroll
-                for (int i = 0; i < 7; ++i) c0[i] = (int32_t)ss(ST_STAT_COUNT0 + i);
+                for (int i = 0; i < 7; ++i) c0[i] = (int32_t)(LCD ? lcc7[i] : ss(ST_STAT_COUNT0 + i));
                 const int pk = draw_shape<kWin, false>(need1, c0, mtst, p.mt + e0 * kMtPitch, sm.S, lane, pre, false);
                 if (need1) {
                     sid = pk;
@@ -1457,15 +1506,13 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 }
                 dpar = draw_par(cnt);
             }
-            if constexpr (TWO) {
-                sm.pick1[lane] = (uint32_t)sid;
-                if (lane == 0) lds_flag_set(&sm.f2, (uint32_t)t + 1u);
-            }
+            sm.pick1[lane] = (uint32_t)sid;
+            if (lane == 0) lds_flag_set(&sm.f2, (uint32_t)t + 1u);
             const uint32_t m0 = mtst;
             const int npv = draw_core<kWin>(dr_spec, dpar, mtst, p.mt + e0 * kMtPitch, sm.S, lane, pre,
                                             want_pre && pv_ok(mt0));
             mt_new = pv_pack(mtst, npv, mt_consumed(m0, mtst));
-        } else if constexpr (TWO) {
+        } else {
             sm.pick1[lane] = (uint32_t)sid;
             if (lane == 0) lds_flag_set(&sm.f2, (uint32_t)t + 1u);
         }
@@ -1481,15 +1528,12 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         }
         // commit: lanes whose lock consumed the preview
         bool dr = draw;
-        if constexpr (TWO) {
-            dr = locknow;
-            if (p.autoreset != ST_AUTORESET_SAME_STEP) {
-                lds_flag_wait(&sm.f1, (uint32_t)t + 1u);
-                const uint32_t w = lane < 32 ? sm.drawm[0] : sm.drawm[1];
-                dr = (w >> (lane & 31)) & 1u;
-            }
+        dr = locknow;
+        if (p.autoreset != ST_AUTORESET_SAME_STEP) {
+            lds_flag_wait(&sm.f1, (uint32_t)t + 1u);
+            const uint32_t w = lane < 32 ? sm.drawm[0] : sm.drawm[1];
+            dr = (w >> (lane & 31)) & 1u;
         }
-        [[maybe_unused]] uint32_t sdd = 0;
         // (a lane that locks but does not draw -- a death without auto-reset
         // -- keeps its old MT word: its speculative draw is dropped)
         uint32_t mt_out = dr ? mt_new : mt0;
@@ -1518,36 +1562,20 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                         real ? ((uint32_t)(ST_STAT_COUNT0 + i) * (uint32_t)p.n + (uint32_t)e) * 4u : kOff, 0, kNT);
             }
         } else {
-            if (dr || chunk_me) {
-                ss(ST_STAT_MT_INDEX) = mt_out;
-                sdd = 1u << ST_STAT_MT_INDEX;
-            }
-            if (dr) {
-                atomicAdd(&ss(ST_STAT_COUNT0 + sid), 1u);  // shape_counts[name] += 1, :199 (ds_add, no return)
-                sdd |= 1u << (ST_STAT_COUNT0 + sid);
-            }
-        }
-        if constexpr (KSTEPS == 1) {
-            if constexpr (STEP2) (void)sdd;  // (stored above)
-            else sm.SD[lane] = sdd;  // the logic part ORs its rows in below
-        } else if constexpr (TWO) {
+            // rollout: the staged rows (stored at the end of the launch)
+            if (dr || chunk_me) ss(ST_STAT_MT_INDEX) = mt_out;
+            if (dr) atomicAdd(&ss(ST_STAT_COUNT0 + sid), 1u);  // shape_counts[name] += 1, :199 (ds_add, no return)
             sm.mtw[t & 1][lane] = mt_out;  // the logic wave's next step reads it after B1
         }
         ST_STAMP(11);
     }
 
     if constexpr (DO_L) {
-        if constexpr (TWO) {
-            // a spawn without a preview takes the draw wave's first draw (rare)
-            const bool need1 = draw && !pv_ok(mt0);
-            if (__ballot(need1)) {
-                lds_flag_wait(&sm.f2, (uint32_t)t + 1u);
-                if (need1) sid = (int)sm.pick1[lane];
-                if constexpr (KSTEPS == 1 && !OVP) {  // its overlay (the others were painted with the board stores)
-                    const uint2 sd1 = tab(sid * 4);
-                    paint<S32>(L, lane, sd1.x, sd1.y, W / 2, 0, need1 && spawn ? hmask : 0u);
-                }
-            }
+        // a spawn without a preview takes the draw wave's first draw (rare)
+        const bool need1 = draw && !pv_ok(mt0);
+        if (__ballot(need1)) {
+            lds_flag_wait(&sm.f2, (uint32_t)t + 1u);
+            if (need1) sid = (int)sm.pick1[lane];
         }
         ST_STAMP(4);
         uint32_t pw_out = pack_piece(id, rot, ax, ay, lock);
@@ -1559,6 +1587,21 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         }
 
         // ---- counters back to the staged rows (tetris_env.py:253, :264-299) ----
+        if constexpr (LCL) {
+            // the late-loaded counters (issued before B1; the lock path kept
+            // deltas) -- absolute values and the old ones for the dirty tests
+            if (locknow) {
+                o_score = (int32_t)lcv[0];
+                o_lines = (int32_t)lcv[1];
+                o_holes = (int32_t)lcv[2];
+                o_height = (int32_t)lcv[3];
+                o_deaths = (int32_t)lcv[4];
+                score += o_score;
+                lines += o_lines;
+                deaths += o_deaths;
+                if (!hset) height = o_height;
+            }
+        }
         [[maybe_unused]] int32_t ep_t = 0, ep_s = 0, ep_l = 0, ep_h = 0;  // VEC: info's ep_* rows
         if constexpr (VEC) {
             if (reset_now) {
@@ -1576,8 +1619,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             st[ST_STAT_EP_HOLES * sd] = holes;
             time = score = lines = holes = height = 0;
         }
-        // st_step stores only the counter rows that changed (sdirty, per env)
-        [[maybe_unused]] uint32_t sdirty = (1u << ST_STAT_TIME) | (1u << kPieceRow);
+        // st_step stores only the counter rows that changed (per env)
         if constexpr (STEP2) {
             // st_step: straight from the registers, one coalesced dword per
             // lane and changed row (no staging through LDS at the end of the
@@ -1621,10 +1663,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             ss(ST_STAT_TIME) = (uint32_t)time;
             ss(kPieceRow) = pw_out;
             if (locknow) {
-                auto put = [&](int r, int32_t v, int32_t old) {
-                    if constexpr (KSTEPS == 1) sdirty |= (uint32_t)(old != v) << r;
-                    ss(r) = (uint32_t)v;
-                };
+                auto put = [&](int r, int32_t v, int32_t) { ss(r) = (uint32_t)v; };
                 put(ST_STAT_SCORE, score, o_score);
                 put(ST_STAT_LINES, lines, o_lines);
                 put(ST_STAT_HOLES, holes, o_holes);
@@ -1632,10 +1671,9 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 put(ST_STAT_DEATHS, deaths, o_deaths);
             }
         }
-        if constexpr (KSTEPS == 1 && !STEP2) sm.SD[lane] |= sdirty;
 
         // ---- observation (tetris_env.py:301-302): board + current piece ----
-        if constexpr (!(KSTEPS == 1 && TWO)) {
+        if constexpr (KSTEPS != 1) {
             if (KSTEPS != 1 || spawn) paint<S32>(L, lane, odesc.x, odesc.y, oax, oay, hmask);
         }
         wave_sync();
@@ -1673,6 +1711,37 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                     __builtin_amdgcn_raw_buffer_store_b32(fin ? 0u : v, ro, off, 0, kNT);
                     if constexpr (VEC) __builtin_amdgcn_raw_buffer_store_b32(v, rf, fin ? off : kOff, 0, kNT);
                 }
+            }
+        }
+        if constexpr (KSTEPS == 1) {
+            if (p.wire) {
+                // st_step_wire (BASELINE C5's gather format, st_wire_words):
+                // per env one bit stream -- column x's H obs bits at bit x*H,
+                // then the reward's low 16 bits (|reward| < 2^15 for W <= 32,
+                // H <= 28) and done -- as words [j][n], so one gather moves
+                // ceil((W*H + 17) / 32) words per env (10x20: 7, 28 B) instead
+                // of obs + reward + done as W + 2 words (48 B)
+                const auto rw = buf_rsrc(p.wire, (uint32_t)((W * H + 17 + 31) / 32) * (uint32_t)p.n * 4u);
+                uint32_t off = (uint32_t)e * 4u;
+                const uint32_t rowb = (uint32_t)p.n * 4u;
+                uint64_t acc = 0;
+                int nb = 0;
+                auto put = [&](uint32_t bits, int k) {  // k <= 32
+                    acc |= (uint64_t)bits << nb;
+                    nb += k;
+                    if (nb >= 32) {
+                        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)acc, rw, real ? off : kOff, 0, kNT);
+                        off += rowb;
+                        acc >>= 32;
+                        nb -= 32;
+                    }
+                };
+#pragma unroll
+                for (int x = 0; x < (WT ? WT : kMaxW); ++x)
+                    if (WT || x < W) put((lcol(L, x, lane) | lcol(sm.OV, x, lane)) & hmask, H);
+                put((uint32_t)rew & 0xFFFFu, 16);
+                put(died ? 1u : 0u, 1);
+                if (nb > 0) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)acc, rw, real ? off : kOff, 0, kNT);
             }
         }
         if (F32) {
@@ -1768,20 +1837,11 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             }
         }
     }
-    // counter rows: all (rollout) or those one of the lane's 4 envs changed;
-    // two waves: each stores the rows it owns (logic: 0-5 and the piece row,
-    // draw: the shape counts and the MT word)
-    uint32_t sdl = ~0u;
-    if constexpr (STEP2) {
-        // (stored per lane above)
-    } else if constexpr (KSTEPS == 1) {
-        const uint32_t *sdm = ROLE == kRoleD ? sm.SDD : sm.SD;
-        const uint4 sd4 = *reinterpret_cast<const uint4 *>(&sdm[lcc]);
-        sdl = (sd4.x | sd4.y | sd4.z | sd4.w) >> lrow;
-    }
+    // rollout: the staged counter rows, each wave the rows it owns (logic:
+    // 0-5 and the piece row, draw: the shape counts and the MT word); st_step
+    // stored its changed rows per lane above
     constexpr uint32_t kRowsD = ((1u << 7) - 1u) << ST_STAT_COUNT0 | 1u << ST_STAT_MT_INDEX;
-    constexpr uint32_t kOwn = ROLE == kRoleOne ? (1u << kHotRows) - 1u
-                              : ROLE == kRoleD ? kRowsD : ((1u << kHotRows) - 1u) & ~kRowsD;
+    constexpr uint32_t kOwn = ROLE == kRoleD ? kRowsD : ((1u << kHotRows) - 1u) & ~kRowsD;
     const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
     const uint32_t soff = (uint32_t)e0 * 4u + loff * 4u;
 #pragma unroll
@@ -1789,7 +1849,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         if constexpr (STEP2) break;
         // row 15 (ep_time) is never staged: it is stored per lane on a reset
         if (((kOwn >> (4 * q)) & 0xFu) == 0u) continue;
-        const bool st = ((kOwn >> (4 * q + lrow)) & 1u) && ((sdl >> (4 * q)) & 1u);
+        const bool st = (kOwn >> (4 * q + lrow)) & 1u;
         buf_store16<kNT>(rs, st ? soff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff,
                          *reinterpret_cast<const uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]));
     }
@@ -1883,21 +1943,11 @@ __global__ __launch_bounds__(2 * kWave) void k_step(KParams p) {
 // reference state (before q0's draw) is in the generation q1 ended in, so it
 // never overwrites words a committed preview may give back.
 constexpr int kRoleO = 3;
-// issue priorities of the rollout's waves (A/B knobs)
-// (the logic wave's chain sets the step: at 3 against 0, -6% per step,
-// tools/ab_libs_ro.sh)
-#ifndef ST_RO_LPRIO
-#define ST_RO_LPRIO 3
-#endif
-#ifndef ST_RO_DPRIO
-#define ST_RO_DPRIO ST_DPRIO
-#endif
-#ifndef ST_RO_OPRIO
-#define ST_RO_OPRIO 0
-#endif
-#ifndef ST_RO_CHO
-#define ST_RO_CHO 1
-#endif
+// issue priority of the rollout's logic wave (its chain sets the step: 3
+// against 0, -6% per step; logic 0-3 x draw 0-2 measured in round 3,
+// profiles/r03/ro_ab_priorities.txt); the draw wave runs at kDrawPrio after
+// its first round, the output wave at 0
+constexpr int kRoLogicPrio = 3;
 template <int WT, bool F32>
 struct RoLds {
     static constexpr int kCols = (WT ? WT : kMaxW) + 2 * kPad;
@@ -1934,7 +1984,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
     // the next-generation chunks: built by the output wave with packed obs
     // (it idles most of a step), by the draw wave with float32 obs (the
     // output wave's stores set that step)
-    constexpr bool CHO = !F32 && ST_RO_CHO;
+    constexpr bool CHO = !F32;
     const uint32_t kFlags = SC0 ? (p.flags & (ST_REWARD_STEP | ST_STEP_RESET)) : p.flags;
 #if defined(ST_ABLATION) && ST_ABLATION
     const uint32_t kAblate = p.ablate;
@@ -2057,8 +2107,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
     }
     wg_barrier();  // B0
     stamp(0);
-    if constexpr (ROLE == kRoleL && ST_RO_LPRIO > 0) __builtin_amdgcn_s_setprio(ST_RO_LPRIO);
-    if constexpr (ROLE == kRoleO && ST_RO_OPRIO > 0) __builtin_amdgcn_s_setprio(ST_RO_OPRIO);
+    if constexpr (ROLE == kRoleL) __builtin_amdgcn_s_setprio(kRoLogicPrio);
 
     if constexpr (ROLE == kRoleL) {
         // ================================================================ logic
@@ -2143,8 +2192,8 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 for (;;) {
                     const uint32_t fdv = lds_flag_get(&sm.fd), fqv = lds_flag_get(&sm.fq);
                     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-                    act_n = sm.act[(t + 1) & 3][lane];
-                    qwd = sm.qring[lane];
+                    act_n = lds_ld(&sm.act[(t + 1) & 3][lane]);
+                    qwd = lds_ld(&sm.qring[lane]);
                     __atomic_signal_fence(__ATOMIC_SEQ_CST);
                     const bool ok_d = (kAblate & 160u) || (int32_t)(fdv - need_d) >= 0;
                     const bool ok_q = (kAblate & 288u) || (int32_t)(fqv - (uint32_t)t) >= 0;
@@ -2266,8 +2315,8 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             {
                 const uint64_t m = __ballot(draw);
                 if (lane == 0) {
-                    sm.cm[t & 1][0] = (uint32_t)m;
-                    sm.cm[t & 1][1] = (uint32_t)(m >> 32);
+                    lds_st(&sm.cm[t & 1][0], (uint32_t)m);
+                    lds_st(&sm.cm[t & 1][1], (uint32_t)(m >> 32));
                     lds_flag_set(&sm.fl, (uint32_t)t + 1u);
                 }
             }
@@ -2402,7 +2451,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
         sm.act[2][lane] = a2;
         sm.act[3][lane] = a3;
         if (lane == 0) lds_flag_set(&sm.fd, 1u);
-        if constexpr (ST_RO_DPRIO > 0) __builtin_amdgcn_s_setprio(ST_RO_DPRIO);
+        __builtin_amdgcn_s_setprio(kDrawPrio);
         bool rl = false;  // wn holds a reload to merge
         for (int s = 0; s < K; ++s) {
             stamp(1);
@@ -2437,7 +2486,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             for (;;) {
                 const uint32_t f = lds_flag_get(&sm.fl);
                 __atomic_signal_fence(__ATOMIC_SEQ_CST);
-                w = lane < 32 ? sm.cm[s & 1][0] : sm.cm[s & 1][1];
+                w = lds_ld(&sm.cm[s & 1][lane < 32 ? 0 : 1]);
                 __atomic_signal_fence(__ATOMIC_SEQ_CST);
                 if ((int32_t)(f - ((uint32_t)s + 1u)) >= 0) break;
                 __builtin_amdgcn_s_sleep(1);
@@ -2465,7 +2514,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 qw = (qw & ~(0xFu << sh)) | ((uint32_t)pk << sh);
                 nd += 1u;
             }
-            sm.qring[lane] = qw;
+            lds_st(&sm.qring[lane], qw);
             if (lane == 0) lds_flag_set(&sm.fd, (uint32_t)s + 2u);
             stamp(3);
             [[maybe_unused]] int chunk_pg = 0;
@@ -2497,7 +2546,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 wlim = wlim_n;
             }
             rl = cons;
-            sm.act[s & 3][lane] = an;  // step s + 4's (the logic wave has read step s's)
+            lds_st(&sm.act[s & 3][lane], an);  // step s + 4's (the logic wave has read step s's)
             mt_pre_load<kMtWin>(mrs, mta, rl, wn);
             o_rl = o;
             wlim_n = win_lim(mta);
@@ -3516,6 +3565,42 @@ hipError_t launch_rollout(const KParams &p, hipStream_t s) {
         if (f32) hipLaunchKernelGGL((k_rollout<0, 0, true>), grid, block, 0, s, p);
         else hipLaunchKernelGGL((k_rollout<0, 0, false>), grid, block, 0, s, p);
     }
+    return hipGetLastError();
+}
+
+// st_unwire: the wire format (st_step_wire, above) back to packed obs
+// [W][n], reward [n] (sign-extended from 16 bits) and done [n]; one env per
+// thread, words [j][n] coalesced across the wave
+__global__ __launch_bounds__(256) void k_unwire(int W, int H, int64_t n, const uint32_t *__restrict__ wire,
+                                                uint32_t *__restrict__ obs, int32_t *__restrict__ reward,
+                                                uint8_t *__restrict__ done) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const uint32_t hm = (1u << H) - 1u;
+    const uint32_t *src = wire + e;
+    uint64_t acc = 0;
+    int nb = 0;
+    auto take = [&](int k) -> uint32_t {  // k <= 32
+        if (nb < k) {
+            acc |= (uint64_t)*src << nb;
+            src += n;
+            nb += 32;
+        }
+        const uint32_t v = (uint32_t)acc & (k == 32 ? ~0u : (1u << k) - 1u);
+        acc >>= k;
+        nb -= k;
+        return v;
+    };
+    for (int x = 0; x < W; ++x) obs[(int64_t)x * n + e] = take(H) & hm;
+    reward[e] = (int32_t)(int16_t)(uint16_t)take(16);
+    done[e] = (uint8_t)take(1);
+}
+
+hipError_t launch_unwire(int W, int H, int64_t n, const uint32_t *wire, uint32_t *obs, int32_t *reward,
+                         uint8_t *done, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_unwire, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, W, H, n, wire, obs, reward,
+                       done);
     return hipGetLastError();
 }
 

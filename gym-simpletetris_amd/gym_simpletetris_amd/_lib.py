@@ -37,6 +37,7 @@ MT_N = 624
 EXPORT_MT, EXPORT_OBS_F32 = 1, 2  # st_export_env parts
 
 EXPORTS = ("st_create", "st_destroy", "st_seed", "st_reset", "st_step", "st_step_f32", "st_step_vec", "st_rollout",
+           "st_wire_words", "st_step_wire", "st_unwire",
            "st_obs_to_f32", "st_render", "st_grayscale", "st_state", "st_copy", "st_mt_sync", "st_state_bytes", "st_save",
            "st_load", "st_export_env", "st_export_words", "st_check_actions", "st_set_action_flag", "st_stream_sync",
            "st_host_device_ptr", "st_gen_actions", "st_policy_greedy", "st_debug_stamps", "st_last_error", "st_abi_version")
@@ -88,6 +89,9 @@ def load(path: str = LIB_PATH):
         "st_step_f32": ([vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "st_step_vec": ([vp, vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "st_rollout": ([vp, i32, vp, vp, vp, vp, vp, vp], ctypes.c_int),
+        "st_wire_words": ([i32, i32], ctypes.c_int),
+        "st_step_wire": ([vp, vp, vp, vp], ctypes.c_int),
+        "st_unwire": ([i32, i32, i64, vp, vp, vp, vp, vp], ctypes.c_int),
         "st_obs_to_f32": ([vp, vp, vp, vp], ctypes.c_int),
         "st_render": ([vp, vp, vp], ctypes.c_int),
         "st_grayscale": ([vp, vp, i32, i32, i32, vp, vp], ctypes.c_int),
@@ -120,6 +124,13 @@ def load(path: str = LIB_PATH):
         raise ImportError(f"libsimpletetris ABI {L.st_abi_version()} != 1")
     _lib = L
     return L
+
+
+def check_count(rc: int) -> int:
+    """A non-negative count, or the library's error for a negative code."""
+    if rc < 0:
+        check(rc)
+    return rc
 
 
 def check(rc: int):

@@ -14,6 +14,13 @@ rows 0..W-1 packed obs words, row W reward, row W+1 done bytes.  Collective
 gathers need one size on every rank, so when n_global % world != 0 the short
 ranks pad their buffer to the longest shard (`shard_cap`) for the transfer and
 `assemble` drops the padding columns again.
+
+With `wire=True` (ShardedTetris) each rank steps with st_step_wire straight
+into a [wire_words][n_local] int32 buffer -- per env one bit stream of the
+obs columns, the reward's low 16 bits and done: 7 words (28 B) per 10x20 env
+instead of W + 2 (48 B), so the per-step gather moves 1.7x fewer bytes into
+rank 0 -- and rank 0 turns the gathered rows back into (obs, reward, done)
+with st_unwire (`assemble_wire`), bit-exact.
 """
 from __future__ import annotations
 
@@ -85,11 +92,28 @@ def assemble(bufs: List[torch.Tensor], width: int, counts: Optional[List[int]] =
     return obs, reward, done
 
 
+def assemble_wire(bufs: List[torch.Tensor], width: int, height: int,
+                  counts: Optional[List[int]] = None):
+    """Rank-0 side of the wire format: gathered [words][n_cap] int32 buffers
+    (any device; unpacked on the GPU by st_unwire, on `device` or the
+    buffers' own) -> global (obs [W][N], reward [N], done [N]) in global env
+    order, on the GPU."""
+    from .engine import unwire
+    counts = [b.shape[1] for b in bufs] if counts is None else counts
+    if len(counts) != len(bufs):
+        raise ValueError(f"{len(counts)} counts for {len(bufs)} buffers")
+    dev = next((b.device for b in bufs if b.device.type == "cuda"), None)
+    if dev is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    wire = torch.cat([b[:, :c].to(dev) for b, c in zip(bufs, counts)], dim=1).contiguous()
+    return unwire(wire, width, height)
+
+
 class ShardedTetris:
     """This rank's shard of a global batch of `n_global` envs."""
 
     def __init__(self, n_global: int, seed: int = 0, rank: Optional[int] = None,
-                 world: Optional[int] = None, device=None, **engine_kwargs):
+                 world: Optional[int] = None, device=None, wire: bool = False, **engine_kwargs):
         from .engine import TetrisBatch
         self.rank = dist.get_rank() if rank is None else rank
         self.world = dist.get_world_size() if world is None else world
@@ -102,8 +126,13 @@ class ShardedTetris:
         self.engine = TetrisBatch(self.n, device=device,
                                   seeds=[seed + self.offset + e for e in range(self.n)],
                                   **engine_kwargs)
-        self.buf = output_buffer(self.engine.width, self.n, self.engine.device)
-        self._obs, self._rew, self._done = buffer_views(self.buf, self.engine.width)
+        self.wire = bool(wire)
+        if self.wire:  # st_step_wire's rows (see the module docstring)
+            self.buf = torch.zeros((self.engine.wire_words, self.n), dtype=torch.int32,
+                                   device=self.engine.device)
+        else:
+            self.buf = output_buffer(self.engine.width, self.n, self.engine.device)
+            self._obs, self._rew, self._done = buffer_views(self.buf, self.engine.width)
 
     def reset(self):
         self.engine.reset()
@@ -112,7 +141,11 @@ class ShardedTetris:
         """Step the shard, writing straight into the gather buffer (the
         engine's own action checks apply: shape, dtype, device, and 0..6 --
         by default in the step kernel, so a KeyError for an out-of-range
-        device action comes at the next step or engine.check_actions())."""
+        device action comes at the next step or engine.check_actions()).
+        Returns (obs, reward, done) views of the buffer, or with wire=True the
+        buffer itself (the wire rows)."""
+        if self.wire:
+            return self.engine.step_wire(actions, out=self.buf)
         return self.engine.step(actions, obs="packed", out=(self._obs, self._rew, self._done))
 
     def gather(self, dst: int = 0, cpu: bool = False):
@@ -123,4 +156,6 @@ class ShardedTetris:
 
     def assemble(self, bufs: List[torch.Tensor]):
         """Global (obs [W][N], reward [N], done [N]) from gather()'s result."""
+        if self.wire:
+            return assemble_wire(bufs, self.engine.width, self.engine.height, self.counts)
         return assemble(bufs, self.engine.width, self.counts)

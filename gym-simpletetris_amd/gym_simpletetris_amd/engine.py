@@ -312,6 +312,27 @@ class TetrisBatch:
                                 _ptr(r_t), _ptr(d_t), s))
         return (o_t if obs == "packed" else None), r_t, d_t
 
+    @property
+    def wire_words(self) -> int:
+        """uint32 rows per env of the gather format (st_wire_words)."""
+        return C.check_count(self._L.st_wire_words(self.width, self.height))
+
+    def step_wire(self, actions, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One step (as step()) writing BASELINE C5's gather format instead
+        of obs / reward / done: int32 [wire_words, n], per env column x's obs
+        bits at bit x*H, then the reward's low 16 bits and done
+        (st_step_wire; `unwire` restores step()'s outputs bit-exactly)."""
+        a = self._actions(actions)
+        shape = (self.wire_words, self.n)
+        if out is None:
+            out = torch.empty(shape, dtype=torch.int32, device=self.device)
+        elif out.device != self.device or tuple(out.shape) != shape or out.dtype != torch.int32 \
+                or not out.is_contiguous():
+            raise ValueError(f"out tensor {tuple(out.shape)} {out.dtype} on {out.device}: "
+                             f"need contiguous int32 {shape} on {self.device}")
+        C.check(self._L.st_step_wire(self._ctx, _ptr(a), _ptr(out), self._stream()))
+        return out
+
     def rollout(self, actions: torch.Tensor, obs: str = "packed", out: Optional[dict] = None):
         """K consecutive steps in one kernel launch (st_rollout).
 
@@ -492,3 +513,23 @@ class TetrisBatch:
             C.check(self._L.st_gen_actions(_ptr(out), self.n, int(t), ctypes.c_uint64(seed),
                                            int(global_offset), self._stream()))
         return out
+
+
+def unwire(wire: torch.Tensor, width: int, height: int):
+    """st_unwire: gathered wire rows int32 [words, n] (st_step_wire, one
+    shard's or several shards' concatenated along n) on a GPU -> (packed obs
+    int32 [width, n], reward int32 [n], done bool [n]), bit-exact with
+    step()'s outputs.  Runs on the tensor's device, on torch's current stream."""
+    L = C.load()
+    words = C.check_count(L.st_wire_words(width, height))
+    if not isinstance(wire, torch.Tensor) or wire.device.type != "cuda" or wire.dtype != torch.int32 \
+            or wire.dim() != 2 or wire.shape[0] != words or not wire.is_contiguous():
+        raise ValueError(f"wire must be a contiguous int32 [{words}, n] GPU tensor")
+    n = wire.shape[1]
+    obs = torch.empty((width, n), dtype=torch.int32, device=wire.device)
+    reward = torch.empty(n, dtype=torch.int32, device=wire.device)
+    done = torch.empty(n, dtype=torch.bool, device=wire.device)
+    with torch.cuda.device(wire.device):
+        C.check(L.st_unwire(width, height, n, _ptr(wire), _ptr(obs), _ptr(reward), _ptr(done),
+                            _stream_ptr(wire.device)))
+    return obs, reward, done

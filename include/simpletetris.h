@@ -172,6 +172,24 @@ int st_step_vec(st_ctx *ctx, const uint8_t *d_actions, uint32_t *d_obs, float *d
                 int32_t *d_reward, uint8_t *d_done, uint32_t *d_final_obs, int32_t *d_info,
                 st_stream stream);
 
+/* BASELINE C5's gather format.  st_step_wire is st_step writing, instead of
+ * obs / reward / done, one bit stream per env: column x's `height` obs bits
+ * (exactly st_step's packed obs word x) at bit x*height, then the reward's
+ * low 16 bits (two's complement; |reward| < 2^15 for every flag set with
+ * width <= 32, height <= 28) and the done bit -- stored as
+ * st_wire_words(width, height) = ceil((width*height + 17) / 32) uint32 rows
+ * d_wire [words][n_envs] (10x20: 7 words, 28 B per env, against 48 B for
+ * obs + reward + done as width + 2 rows), so a per-step gather of every
+ * shard's outputs to rank 0 (tetris_env.py:397-403's return values, for all
+ * envs) moves 1.7x fewer bytes over xGMI.  st_unwire turns gathered wire
+ * rows back into st_step's outputs (d_obs uint32 [width][n], d_reward int32
+ * [n], d_done uint8 [n]), bit-exact.  st_wire_words returns ST_EINVAL for a
+ * board outside 1..32 x 1..28. */
+int st_wire_words(int32_t width, int32_t height);
+int st_step_wire(st_ctx *ctx, const uint8_t *d_actions, uint32_t *d_wire, st_stream stream);
+int st_unwire(int32_t width, int32_t height, int64_t n, const uint32_t *d_wire, uint32_t *d_obs,
+              int32_t *d_reward, uint8_t *d_done, st_stream stream);
+
 /* k consecutive st_step calls in ONE launch: the driver loop of README.md:43-51
  * (`for t: obs, r, done, info = env.step(a[t])`) with all actions known up
  * front (synthetic / replayed rollouts).  Boards and counters stay on chip

@@ -39,6 +39,10 @@ def test_host_only_abi_functions_and_constants():
     assert L.st_abi_version() == 1
     assert L.st_export_words(10, 20) == 10 + 2 + _lib.NSTAT + _lib.MT_N + 200
     assert L.st_export_words(4, 4) == 4 + 2 + _lib.NSTAT + _lib.MT_N + 16
+    # the C5 gather format: ceil((W*H + 17) / 32) words per env
+    assert L.st_wire_words(10, 20) == 7 and L.st_wire_words(32, 28) == 29 and L.st_wire_words(4, 4) == 2
+    assert L.st_wire_words(0, 20) == _lib.ST_EINVAL and L.st_wire_words(10, 29) == _lib.ST_EINVAL
+    assert L.st_unwire(10, 20, -1, None, None, None, None, None) == _lib.ST_EINVAL
     src = open(os.path.join(ROOT, "include", "simpletetris.h")).read()
     defs = dict(re.findall(r"#define\s+(ST_EXPORT_\w+)\s+(\d+)u", src))
     assert int(defs["ST_EXPORT_MT"]) == _lib.EXPORT_MT and int(defs["ST_EXPORT_OBS_F32"]) == _lib.EXPORT_OBS_F32

@@ -181,7 +181,9 @@ def test_bench_gpus8_direct_invocation(tmp_path):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 8 and d["config"]["envs_total"] == 8 * 2048
     assert d["value"] > 0 and d["gather"]["gathers_in_timed_region"] == 20
-    assert d["gather"]["bytes_per_rank_per_step"] == (10 + 2) * 2048 * 4
+    # the default gather format: st_step_wire's 7 rows per env, not W + 2
+    assert d["gather"]["bytes_per_rank_per_step"] == 7 * 2048 * 4
+    assert d["gather"]["format"].startswith("st_step_wire")
     assert d["config"]["workload"].startswith("C5:")
     assert d["scaling"] == "weak"
     z = check_bench_dump(dump, 8 * 2048, 25)

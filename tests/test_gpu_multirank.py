@@ -108,11 +108,13 @@ def check_bench_dump(path, n_global, steps):
 
 
 def test_bench_gpus2_direct_invocation(tmp_path):
+    """bench.py --gpus 2 with the row gather format (st_step's obs / reward /
+    done rows; the 8-rank test covers the default wire format)."""
     env = dict(os.environ, ST_BENCH_SHARED_GPU="1", ST_BENCH_DUMP=str(tmp_path / "c5.npz"))
     env.pop("WORLD_SIZE", None)
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
                         "--steps", "30", "--warmup", "5", "--n-envs", "8192", "--no-cpu-baseline",
-                        "--no-clear-heavy"],
+                        "--no-clear-heavy", "--gather-format", "rows"],
                        env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -120,6 +122,7 @@ def test_bench_gpus2_direct_invocation(tmp_path):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["envs_total"] == 2 * 8192
     assert d["value"] > 0 and d["gather"]["gathers_in_timed_region"] == 30
+    assert d["gather"]["bytes_per_rank_per_step"] == (10 + 2) * 8192 * 4
     assert d["step_no_gather"]["value"] > 0
     assert d["scaling"] == "weak"
     z = check_bench_dump(tmp_path / "c5.npz", 2 * 8192, 35)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Profiling pass for one round's numbers (TAG=r03 bash tools/gpu_prof.sh):
+# Profiling pass for one round's numbers (TAG=r04 bash tools/gpu_prof.sh):
 #  1. rocprofv3 --kernel-trace --stats of the default bench command (all
 #     variants) and of the headline alone (--no-extras: clean per-kernel stats),
 #     plus tools/trace_summary.py per-run splits of both traces and their
@@ -18,7 +18,7 @@
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd /tmp && export TMPDIR=/tmp
-TAG=${TAG:-r03}
+TAG=${TAG:-r04}
 O="$R/gpurun_out"
 mkdir -p "$O"
 B="$R/bench.py"
