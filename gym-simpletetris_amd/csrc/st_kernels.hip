@@ -1259,13 +1259,32 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         // is ctz(v) (H when empty) and its holes are H - ctz(v) - popc(v & hmask):
         // summed, holes = W*H - sum ctz(v) - (sum popc(v) - W*(32-H)).
         uint32_t andv = ~0u, orv = 0, sctz = 0, spop = 0;
+        // (compile-time width: all W column reads issued before any is used,
+        // one LDS round trip -- left to itself the scheduler reused the first
+        // reads' registers as accumulators and issued the last pair after
+        // waiting for the others; the clear path reuses the words)
+        [[maybe_unused]] uint32_t cw[WT ? WT : 1];
+        if constexpr (WT != 0) {
+#pragma unroll
+            for (int x = 0; x < WT; ++x) cw[x] = lcol(L, x, lane);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int x = 0; x < WT; ++x) {
+                const uint32_t v = cw[x];
+                andv &= v;
+                orv |= v;
+                sctz += __builtin_ctz(v);
+                spop += __builtin_popcount(v);
+            }
+        } else {
 #pragma unroll 8
-        for (int x = 0; x < W; ++x) {
-            const uint32_t v = lcol(L, x, lane);
-            andv &= v;
-            orv |= v;
-            sctz += __builtin_ctz(v);
-            spop += __builtin_popcount(v);
+            for (int x = 0; x < W; ++x) {
+                const uint32_t v = lcol(L, x, lane);
+                andv &= v;
+                orv |= v;
+                sctz += __builtin_ctz(v);
+                spop += __builtin_popcount(v);
+            }
         }
         andv &= hmask;
         if constexpr (KSTEPS == 1) {
@@ -1284,7 +1303,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 // the wave's largest clear count, not one loop per column
                 uint32_t c[WT];
 #pragma unroll
-                for (int x = 0; x < WT; ++x) c[x] = lcol(L, x, lane) & hmask;
+                for (int x = 0; x < WT; ++x) c[x] = cw[x] & hmask;
                 uint32_t full = andv;
                 while (full) {
                     const int r = __builtin_ctz(full);
@@ -2148,6 +2167,18 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             uint32_t cur[4], cand[4];
             read_cols(L, lane, desc.y, ax, cur);
             read_cols(L, lane, cdesc.y, cx, cand);
+            // the queue / planes hand-off, read optimistically in the same
+            // LDS round trip as the columns: both counters, step t + 1's
+            // action and the queue word; taken after the action phase if
+            // the counters allow it, else polled there (round 4: one LDS
+            // round trip less per step when the other waves are ahead;
+            // 65,536 envs 1.389 -> 1.382 us/step over 3 alternating rounds,
+            // profiles/r04/ab_colbatch_earlyq.txt)
+            const uint32_t fdv0 = lds_flag_get(&sm.fd), fqv0 = lds_flag_get(&sm.fq);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            const uint32_t act_n0 = lds_ld(&sm.act[(t + 1) & 3][lane]);
+            const uint32_t qwd0 = lds_ld(&sm.qring[lane]);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
             const bool ok = tries && !collides_v<S32>(cdesc.x, ay, cand);
             ax = ok ? cx : ax;
             rot = ok ? cr : rot;
@@ -2187,8 +2218,12 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             // draw wave's mask wait): step t + 1's action (a stale row past
             // the last step: unused) and the queue word
             uint32_t qwd;
-            {
-                const uint32_t need_d = t > 1 ? (uint32_t)t : 1u;
+            const uint32_t need_d = t > 1 ? (uint32_t)t : 1u;
+            if (((kAblate & 160u) || (int32_t)(fdv0 - need_d) >= 0) &&
+                ((kAblate & 288u) || (int32_t)(fqv0 - (uint32_t)t) >= 0)) {
+                act_n = act_n0;
+                qwd = qwd0;
+            } else {
                 for (;;) {
                     const uint32_t fdv = lds_flag_get(&sm.fd), fqv = lds_flag_get(&sm.fq);
                     __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -2214,10 +2249,14 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 paint<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
                 uint32_t andv = ~0u, orv = 0, sctz = 0, spop = 0;
                 if constexpr (WT != 0) {
+                    // all column reads before any use: one LDS round trip (see
+                    // run_steps' lock path)
+#pragma unroll
+                    for (int x = 0; x < WT; ++x) tb[x] = col(L, x);
+                    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                     for (int x = 0; x < WT; ++x) {
-                        const uint32_t v = col(L, x);
-                        tb[x] = v;
+                        const uint32_t v = tb[x];
                         andv &= v;
                         orv |= v;
                         sctz += __builtin_ctz(v);
@@ -2242,7 +2281,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                     if constexpr (WT != 0) {
                         uint32_t c[WT];
 #pragma unroll
-                        for (int x = 0; x < WT; ++x) c[x] = col(L, x) & hmask;
+                        for (int x = 0; x < WT; ++x) c[x] = tb[x] & hmask;
                         uint32_t full = andv;
                         while (full) {
                             const int r = __builtin_ctz(full);

@@ -319,7 +319,9 @@ class VecInfo:
 
     The step kernel writes the counters into the slot this info reads, so
     building it costs nothing per step; the env reuses a slot two steps later
-    and copies it into this object first if this info is still alive then."""
+    and copies it into this object first if this info is still alive then
+    (a counter tensor taken out of the info and kept past that is a view of
+    the slot: clone it to keep it)."""
 
     def __init__(self, env: "TetrisVecEnv", slot: _Slot):
         self._env = env
@@ -328,11 +330,14 @@ class VecInfo:
 
     def _detach(self):
         """Own copies of the slot's tensors (the env is about to reuse it;
-        stream-ordered before the step that overwrites it)."""
+        stream-ordered before the step that overwrites it).  A dict already
+        built from the slot is rebuilt from the copies on the next access
+        (its counter tensors were views into the slot)."""
         self._info = self._info.clone()
         self._done = self._done.clone()
         if self._final is not None:
             self._final = self._final.clone()
+        self._cache = None
 
     def _load(self):
         if self._cache is None:

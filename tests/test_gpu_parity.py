@@ -564,12 +564,19 @@ def test_vec_env_surface():
     assert info["time"].shape == (256,)
     assert int(info["deaths"].sum()) > 0
     # an info kept past later steps still describes its own step
-    kept = v.step(torch.zeros(256, dtype=torch.uint8, device=v.device))[3]
+    # (hard drops: some envs finish an episode in the kept step)
+    _, _, kd, kept = v.step(torch.full((256,), 2, dtype=torch.uint8, device=v.device))
+    kd = kd.clone()
     live = {k: x.clone() for k, x in v.engine.info_tensors().items()}   # the state right now
     for _ in range(3):
         v.step(torch.full((256,), 2, dtype=torch.uint8, device=v.device))
-    for k in ("time", "score", "holes", "deaths", "ep_time", "statistics"):
+    for k in ("time", "score", "holes", "deaths", "statistics"):
         assert torch.equal(kept[k], live[k]), k
+    # ep_*: the episode finished in that step where the env was reset in it,
+    # else 0 (the engine's EP rows keep the last finished episode)
+    assert kd.any()
+    for k in ("ep_time", "ep_score", "ep_lines", "ep_holes"):
+        assert torch.equal(kept[k], torch.where(kd, live[k], torch.zeros_like(live[k]))), k
     assert not torch.equal(v.engine.info_tensors()["time"], live["time"])
 
 

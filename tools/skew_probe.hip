@@ -77,12 +77,20 @@ static int run(const char *name, int blocks, int threads, int spin) {
 }
 
 int main() {
-    const int spin = 400;  // 4 us at 100 MHz
+    // st_step's shape (1,024 workgroups of 2 waves, ~17.5 KB LDS each) against
+    // fewer, larger workgroups carrying the same waves (round 4: does the
+    // dispatch ramp scale with the workgroup count?), each wave spinning about
+    // one st_step wave life (2.8 us)
+    const int spin = 280;
     int rc = 0;
-    rc |= run<0>("1 wave/WG, no LDS", 1024, 64, spin);
-    rc |= run<4480>("1 wave/WG, 17.5 KB LDS", 1024, 64, spin);
-    rc |= run<0>("4 waves/WG, no LDS", 256, 256, spin);
-    rc |= run<0>("1 wave/WG, 2 waves/SIMD", 2048, 64, spin);
-    rc |= run<0>("1 wave/WG, no spin", 1024, 64, 0);
+    for (int rep = 0; rep < 2; ++rep) {
+        rc |= run<4480>("2 waves/WG, 17.5 KB LDS (st_step)", 1024, 128, spin);
+        rc |= run<8960>("4 waves/WG, 35 KB LDS", 512, 256, spin);
+        rc |= run<17920>("8 waves/WG, 70 KB LDS", 256, 512, spin);
+        rc |= run<0>("2 waves/WG, no LDS", 1024, 128, spin);
+        rc |= run<0>("4 waves/WG, no LDS", 512, 256, spin);
+        rc |= run<4480>("2 waves/WG, 17.5 KB LDS, no spin", 1024, 128, 0);
+        rc |= run<8960>("4 waves/WG, 35 KB LDS, no spin", 512, 256, 0);
+    }
     return rc;
 }
