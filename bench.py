@@ -357,9 +357,12 @@ def main():
             ev0.record(s)  # first host calls after a stream switch are slow: not inside the region
             ev1.record(s)
             sync_all()
-            t0 = time.perf_counter()
+            # the start event is recorded on the idle stream right before the
+            # region's clock starts (its host call is instrumentation, not a
+            # step: round 3 had it inside the region); the end event goes in
+            # right behind the K launches, while the GPU is still running them
             ev0.record(s)
-            t1 = time.perf_counter()
+            t0 = t1 = time.perf_counter()
             run()
             t2 = time.perf_counter()
             ev1.record(s)
