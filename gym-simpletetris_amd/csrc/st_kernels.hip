@@ -134,14 +134,6 @@ constexpr int kNT = 2;
 // instruction (since the draw parameters moved before B1 its chain is the
 // step: K = 2,000 4.67-4.72 -> 4.64-4.67 us, profiles/r03/ab_step_lprio.txt).
 constexpr int kDrawPrio = 2;
-// st_step's late counters (see run_steps, LCL / LCD): bit 0 the logic
-// wave's lock-path rows (adopted: K = 2,000 4.642-4.643 -> 4.605-4.635 us,
-// steady 4.533-4.539 -> 4.494-4.516), bit 1 the draw wave's shape counts
-// (+6%: its post-B1 chain, window + counts + draw parameters, becomes the
-// step's); profiles/r04/ab_late_counters.txt
-#ifndef ST_LC
-#define ST_LC 1
-#endif
 constexpr int kLogicPrio = 1;
 template <int AUX = 0>
 __device__ __forceinline__ void buf_store16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
@@ -961,13 +953,14 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     // once the lock decision is known (logic: score .. deaths, issued before
     // B1, needed at the end of the lock path; draw: the shape counts, issued
     // with the MT window after B1)
-    // (ST_LC: A/B knob, bit 0 the logic wave's rows, bit 1 the draw wave's)
-    constexpr bool LCL = KSTEPS == 1 && !VEC && (ST_LC & 1);
-    constexpr bool LCD = KSTEPS == 1 && !VEC && (ST_LC & 2);
+    // (round 4, profiles/r04/ab_late_counters.txt: K = 2,000 4.642-4.643 ->
+    // 4.605-4.635 us; reading the draw wave's shape counts late as well was
+    // +6% -- its post-B1 chain, window + counts + draw parameters, became the
+    // step's -- and was dropped)
+    constexpr bool LCL = KSTEPS == 1 && !VEC;
     // staged counter groups (rows 4q .. 4q + 3): logic 0-1, draw 2-3; with
     // late rows only what the other role still reads early
     auto mine_q = [&](int q) {
-        if constexpr (LCD) return !LCL && ROLE == kRoleL && q < 2;
         if constexpr (LCL) return ROLE == kRoleD && q >= 1;
         return (ROLE == kRoleL) == (q < 2);
     };
@@ -1013,8 +1006,6 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         pw_d = p.piece[e];
         tm_d = reinterpret_cast<const uint32_t *>(p.stats)[(int64_t)ST_STAT_TIME * sd + e];
     }
-    [[maybe_unused]] uint32_t mt_d = 0;  // LCD: the MT word per lane (both waves)
-    if constexpr (LCD) mt_d = reinterpret_cast<const uint32_t *>(p.stats)[(int64_t)ST_STAT_MT_INDEX * sd + e];
     // The piece table, lane i = entry i, from immediates (under the load
     // latency; no memory access: a __constant__ load gets sunk by the
     // compiler past the state loads' completion -- one more serialized round
@@ -1108,7 +1099,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     // MT word at the start of the step (the logic wave uses only the preview
     // bits; in a two-wave step the draw wave replaces the row after B1, and in
     // a two-wave rollout it hands step t-1's word over in mtw: read after B1)
-    uint32_t mt0 = LCD ? mt_d : ss(ST_STAT_MT_INDEX);
+    uint32_t mt0 = ss(ST_STAT_MT_INDEX);
     if constexpr (STAMP && KSTEPS == 1) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     ST_STAMP(1);
 
@@ -1188,15 +1179,13 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     if constexpr (DO_D) {
         mrs = mt_res(p.mt + e0 * kMtPitch, lane);
         mt_chunk_issue(mrs, mt0, real && !(kAblate & 2u), lane, chunk);
-        if constexpr (!LCD) {
-            const int s0 = pv_id(mt0);
+        const int s0 = pv_id(mt0);
 #pragma unroll
-            for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)ss(ST_STAT_COUNT0 + i) + (i == s0);  // _new_piece :199
-            csid = cnt[0];
+        for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)ss(ST_STAT_COUNT0 + i) + (i == s0);  // _new_piece :199
+        csid = cnt[0];
 #pragma unroll
-            for (int i = 1; i < 7; ++i) csid = s0 == i ? cnt[i] : csid;
-            dpar = draw_par(cnt);
-        }
+        for (int i = 1; i < 7; ++i) csid = s0 == i ? cnt[i] : csid;
+        dpar = draw_par(cnt);
     }
     if constexpr (DO_L) {
         const uint64_t m = __ballot(locknow);
@@ -1225,16 +1214,6 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     constexpr int kWin = STEP2 ? 8 : 16;
     MtPre pre;
     if constexpr (DO_D) mt_pre_load<kWin>(mrs, mtst, want_pre, pre);
-    // LC: the shape counts of the locking lanes, with the window
-    [[maybe_unused]] uint32_t lcc7[7] = {};
-    if constexpr (LCD && DO_D) {
-        const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
-        const uint32_t eo = (uint32_t)e * 4u;
-#pragma unroll
-        for (int i = 0; i < 7; ++i)
-            lcc7[i] = __builtin_amdgcn_raw_buffer_load_b32(
-                rs, locknow ? eo + (uint32_t)(ST_STAT_COUNT0 + i) * (uint32_t)sd * 4u : kOff, 0, 0);
-    }
 
     // ---------------- logic: lock path (tetris_env.py:263-299) ----------------
     bool died = false, spawn = false;
@@ -1498,15 +1477,6 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         }
         [[maybe_unused]] const uint32_t mt_before = mtst;
         uint32_t mt_new = mtst;
-        if constexpr (LCD) {
-            const int s0 = pv_id(mt0);
-#pragma unroll
-            for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)lcc7[i] + (i == s0);  // _new_piece :199
-            csid = cnt[0];
-#pragma unroll
-            for (int i = 1; i < 7; ++i) csid = s0 == i ? cnt[i] : csid;
-            dpar = draw_par(cnt);
-        }
         if (!(kAblate & 2u)) {
             mt_win_consume<kWin>(pre);
             const bool need1 = dr_spec && !pv_ok(mt0);
@@ -1514,7 +1484,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 // the piece first, with the counts before the spawn
                 int32_t c0[7];
 #pragma unroll
-                for (int i = 0; i < 7; ++i) c0[i] = (int32_t)(LCD ? lcc7[i] : ss(ST_STAT_COUNT0 + i));
+                for (int i = 0; i < 7; ++i) c0[i] = (int32_t)ss(ST_STAT_COUNT0 + i);
                 const int pk = draw_shape<kWin, false>(need1, c0, mtst, p.mt + e0 * kMtPitch, sm.S, lane, pre, false);
                 if (need1) {
                     sid = pk;
