@@ -3073,13 +3073,7 @@ __global__ __launch_bounds__(256) void k_export(KParams p, int64_t env, const ui
 // the concurrently written regions sit closer together than with 16 envs
 // (tools/ab_img.py at 65,536 envs: 84 gray f32 386 -> 356 us, 160 rgb u8
 // 2,350 -> 2,072 us; tools/write_bw.hip shows the same effect on bare stores)
-#ifndef ST_IMG_ENVS
-#define ST_IMG_ENVS 2
-#endif
-#ifndef ST_IMG_SWEEP
-#define ST_IMG_SWEEP 1
-#endif
-constexpr int kImgEnvs = ST_IMG_ENVS;  // envs per block
+constexpr int kImgEnvs = 2;  // envs per block
 constexpr int kMaxImg = 4096;  // largest image side (st_grayscale checks)
 
 template <typename T>
@@ -3247,9 +3241,7 @@ __global__ __launch_bounds__(256) void k_grayscale(const uint32_t *__restrict__ 
 // wave fetches once per iteration (one word per lane, the next iteration's
 // prefetched under the current one's stores) and hands to each element with
 // a lane shuffle.
-#ifndef ST_IMG_GRID
-#define ST_IMG_GRID 1024
-#endif
+constexpr int kImgSweepGrid = 1024;  // workgroups of the sweep (grid-stride)
 constexpr int kImgRuns = 4;  // U: 1-KB runs per wave iteration
 template <typename T, int CH>
 __global__ __launch_bounds__(256) void k_grayscale_sweep(const uint32_t *__restrict__ obs, T *__restrict__ out,
@@ -3629,11 +3621,11 @@ hipError_t launch_grayscale(const KParams &p, const uint32_t *obs, int size, int
     // span at most two envs and the output is 16-B aligned; else per block
     const int V = as_u8 ? 16 : 4;
     const int64_t per = (int64_t)size * size * channels;
-    if (ST_IMG_SWEEP && !as_u8 && channels == 3 && kWave * V * kImgRuns <= per &&
+    if (!as_u8 && channels == 3 && kWave * V * kImgRuns <= per &&
         (reinterpret_cast<uintptr_t>(out) & 15u) == 0 && (p.n * per) % V == 0) {
         const int64_t runs = (p.n * per + kWave * V - 1) / (kWave * V);
         const int64_t want = (runs + 4 * kImgRuns - 1) / (4 * kImgRuns);  // 4 waves per block
-        const dim3 grid((unsigned)(want < ST_IMG_GRID ? want : ST_IMG_GRID)), block(256);
+        const dim3 grid((unsigned)(want < kImgSweepGrid ? want : kImgSweepGrid)), block(256);
         if (as_u8 && channels == 3)
             hipLaunchKernelGGL((k_grayscale_sweep<uint8_t, 3>), grid, block, 0, s, obs, (uint8_t *)out, p.n, p.W,
                                p.H, size);
