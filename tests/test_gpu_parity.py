@@ -1201,3 +1201,36 @@ def test_save_load_snapshot(tmp_path):
         a.load(bytes(bad))                 # not a snapshot
     with pytest.raises(StError):
         a.load(snap[:-4])                  # truncated
+
+
+@pytest.mark.parametrize("lock_delay,step_reset", [(0, False), (2, True), (3, False)])
+def test_host_written_lock_fields(lock_delay, step_reset):
+    """Lock-delay counters a host wrote beyond lock_delay (the reference's
+    `_lock_delay_fn = (x + 1) % (max(lock_delay, 0) + 1)`, tetris_env.py:175,
+    takes any x): st_step and st_rollout against the oracle with the same
+    counters written into both, up to 40 with lock_mod 1, 3 and 4."""
+    G = _engine()
+    n, T = 512, 80
+    kw = dict(width=10, height=20, lock_delay=lock_delay, step_reset=step_reset, penalise_holes_increase=True)
+    seeds = [77 + e for e in range(n)]
+    a = G.TetrisBatch(n, autoreset="same_step", seeds=seeds, **kw)
+    b = G.TetrisBatch(n, autoreset="same_step", seeds=seeds, **kw)
+    a.reset()
+    b.reset()
+    ob = O.OracleBatch(n, seeds, **kw)
+    ob.reset()
+    locks = np.random.default_rng(5).integers(0, 41, n)
+    for eng in (a, b):
+        p = eng.get_state(("piece",))["piece"].astype(np.int64)
+        eng.set_state(piece=(p & ((1 << 17) - 1)) | (locks << 17))
+    for i in range(n):
+        ob.set_state(i, lock=int(locks[i]))
+    acts = O.splitmix64_actions(13, 0, T, n)
+    ref = ob.rollout(acts)
+    ro, rr, rd = b.rollout(torch.as_tensor(acts, device=b.device))
+    for t in range(T):
+        o, r, d = a.step(torch.as_tensor(acts[t], device=a.device), obs="packed")
+        assert np.array_equal(r.cpu().numpy(), ref["reward"][t]), t
+        assert np.array_equal(d.cpu().numpy().astype(np.uint8), ref["done"][t]), t
+        assert np.array_equal(o.cpu().numpy().view(np.uint32).T, ref["obs"][t]), t
+        assert torch.equal(ro[t], o) and torch.equal(rr[t], r) and torch.equal(rd[t], d), t
