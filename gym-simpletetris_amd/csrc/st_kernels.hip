@@ -95,6 +95,61 @@ static_assert(kTab.ok, "every tetromino column must be a contiguous run within [
 __constant__ uint32_t c_tab_m[28] = ST_TAB28(kTab.m);
 __constant__ uint32_t c_tab_g[28] = ST_TAB28(kTab.g);
 
+// The rollout's piece table ("box columns"): a rotation's columns as four
+// consecutive board columns from its leftmost, dx0 = (g & 7) - 3 (at most 0:
+// every shape holds its anchor cell), column c's cells in byte c of m (0:
+// none) and, in bits [3 + 7c, 10 + 7c) of g as a signed field, the row
+// below its lowest cell relative to the anchor (bottom dy + 1; -64 for no
+// cells: a bottom far above the board, which never stops a drop, see
+// drop_box).  One address per descriptor: the four column reads take
+// immediate offsets.
+constexpr PieceTab make_box_tab() {
+    PieceTab t{};
+    t.ok = true;
+    for (int p = 0; p < 7; ++p) {
+        int cx[4] = {}, cy[4] = {};
+        for (int c = 0; c < 4; ++c) {
+            cx[c] = kShapes[p][c][0];
+            cy[c] = kShapes[p][c][1];
+        }
+        for (int r = 0; r < 4; ++r) {
+            int dx0 = 99, dx1 = -99;
+            for (int c = 0; c < 4; ++c) {
+                dx0 = cx[c] < dx0 ? cx[c] : dx0;
+                dx1 = cx[c] > dx1 ? cx[c] : dx1;
+            }
+            if (dx0 < -3 || dx0 > 0 || dx1 - dx0 > 3) t.ok = false;
+            uint32_t m = 0, g = (uint32_t)(dx0 + 3);
+            for (int k = 0; k < 4; ++k) g |= 64u << (3 + 7 * k);
+            for (int k = 0; k < 4; ++k) {
+                int ymin = 99, ymax = -99, cnt = 0;
+                uint32_t bits = 0;
+                for (int c = 0; c < 4; ++c)
+                    if (cx[c] == dx0 + k) {
+                        ++cnt;
+                        ymin = cy[c] < ymin ? cy[c] : ymin;
+                        ymax = cy[c] > ymax ? cy[c] : ymax;
+                        bits |= 1u << (cy[c] + 3);
+                    }
+                if (!cnt) continue;
+                if (cnt != ymax - ymin + 1 || ymin < -3 || ymax > 3) t.ok = false;
+                m |= bits << (8 * k);
+                g = (g & ~(127u << (3 + 7 * k))) | ((uint32_t)(ymax + 1) & 127u) << (3 + 7 * k);
+            }
+            t.m[p * 4 + r] = m;
+            t.g[p * 4 + r] = g;
+            for (int c = 0; c < 4; ++c) {  // rotated(cclk=False): (i, j) -> (j, -i)
+                const int i = cx[c], j = cy[c];
+                cx[c] = j;
+                cy[c] = -i;
+            }
+        }
+    }
+    return t;
+}
+constexpr PieceTab kBox = make_box_tab();
+static_assert(kBox.ok, "every rotation must span at most four columns from dx0 in [-3, 0]");
+
 // Column j of a descriptor: dx, bottom dy, and its cells at anchor row y as
 // board-row bits; cells with y < 0 vanish (is_occupied skips them,
 // tetris_env.py:32-33; _set_piece clips them, :326).
@@ -197,6 +252,44 @@ __device__ __forceinline__ void erase(uint32_t *L, int lane, uint32_t m, uint32_
 #pragma unroll
     for (int j = 0; j < 4; ++j)
         atomicAnd(&L[(x + pc_dx(g, j) + kPad) * kWave + lane], ~(pc_bits<S32>(m, j, y) & hmask));
+}
+
+// Box-column forms of read_cols / drop_v / paint / erase (kBox descriptors).
+// drop_box: q = the row below the column's lowest cell; a column without
+// cells has q = y - 64, so its shift is 0 and its distance ctz(column) + 64
+// - y exceeds every real column's (at most H + 2 - y: the floor bits stop a
+// drop by row H < 32; every column word holds floor or wall bits, so ctz
+// sees a set bit).  7 VALU a column, the first column seeding the minimum.
+__device__ __forceinline__ int box_x0(uint32_t g, int x) { return x + (int)(g & 7u) - 3; }
+__device__ __forceinline__ void read_box(const uint32_t *L, int lane, uint32_t g, int x, uint32_t (&v)[4]) {
+    const uint32_t *c0 = &L[(box_x0(g, x) + kPad) * kWave + lane];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = c0[j * kWave];
+}
+__device__ __forceinline__ int drop_box(uint32_t g, int y, const uint32_t (&v)[4]) {
+    int dist = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int q = y + ((int32_t)(g << (32 - 10 - 7 * j)) >> 25);  // v_bfe_i32
+        const int s = q > 0 ? q : 0;
+        const int k = __builtin_ctz(v[j] & (~0u << s)) - q;
+        dist = j == 0 || k < dist ? k : dist;
+    }
+    return dist;
+}
+template <bool S32 = false>
+__device__ __forceinline__ void paint_box(uint32_t *L, int lane, uint32_t m, uint32_t g, int x, int y,
+                                          uint32_t hmask) {
+    uint32_t *c0 = &L[(box_x0(g, x) + kPad) * kWave + lane];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) atomicOr(&c0[j * kWave], pc_bits<S32>(m, j, y) & hmask);  // ds_or_b32
+}
+template <bool S32 = false>
+__device__ __forceinline__ void erase_box(uint32_t *L, int lane, uint32_t m, uint32_t g, int x, int y,
+                                          uint32_t hmask) {
+    uint32_t *c0 = &L[(box_x0(g, x) + kPad) * kWave + lane];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) atomicAnd(&c0[j * kWave], ~(pc_bits<S32>(m, j, y) & hmask));
 }
 
 // _clear_lines row compaction (tetris_env.py:205-216) on one column word:
@@ -743,6 +836,15 @@ __device__ __forceinline__ int win_lim(uint32_t m) {
     return l < kMtWin ? l : kMtWin;
 }
 
+// (x + 1) % lock_mod for l1 = x + 1 >= 1 (tetris_env.py:175): l1 <= lock_mod
+// except after a host-written state (a lock field up to 2^15), which the loop
+// reduces; it exits at once for every other lane.  (As a plain % the
+// division ran, exec-masked, on every step.)
+__device__ __forceinline__ int lock_next(int l1, int lock_mod) {
+    int r = l1 < lock_mod ? l1 : l1 - lock_mod;
+    while (r >= lock_mod) r -= lock_mod;
+    return r;
+}
 __device__ __forceinline__ uint32_t pack_piece(int id, int rot, int ax, int ay, int lock) {
     return (uint32_t)id | ((uint32_t)rot << 3) | ((uint32_t)ax << 5) | ((uint32_t)ay << 11) |
            ((uint32_t)lock << 17);
@@ -1115,7 +1217,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         // LDS round trip each; the collision and drop tests are then pure VALU.
         const bool tries = act == 0u || act == 1u || act == 4u || act == 5u;
         const int cx = ax + (act == 0u ? -1 : (act == 1u ? 1 : 0));
-        const int cr = act == 4u ? ((rot + 1) & 3) : (act == 5u ? ((rot + 3) & 3) : rot);
+        const int cr = (rot + (act == 4u ? 1 : 0) + (act == 5u ? 3 : 0)) & 3;  // (selects: the ternary chain became an exec-mask branch)
         desc = tab(id * 4 + rot);
         const uint2 cdesc = tab(id * 4 + cr);
         if constexpr (OVP && DO_L) pd_pv = tab(pv_id(mt0) * 4);
@@ -1149,7 +1251,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         rew = (kFlags & ST_REWARD_STEP) ? 1 : 0;
         if (d == 0) {
             const int l1 = lock + 1;  // (x + 1) % lock_mod; x < lock_mod unless set_state said otherwise
-            lock = l1 < p.lock_mod ? l1 : (l1 == p.lock_mod ? 0 : l1 % p.lock_mod);
+            lock = lock_next(l1, p.lock_mod);
             locknow = lock == 0 && !(kAblate & 1u);
         }
     }
@@ -1408,9 +1510,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         sm.KM[lane] = reset_now ? 0u : hmask;
         sm.BD[lane] = bdirty;
         wave_sync();
-        const uint4 km = *reinterpret_cast<const uint4 *>(&sm.KM[lcc]);
-        const uint4 bd4 = *reinterpret_cast<const uint4 *>(&sm.BD[lcc]);
-        const uint32_t bdl = (bd4.x | bd4.y | bd4.z | bd4.w) >> lrow;
+        uint4 km = *reinterpret_cast<const uint4 *>(&sm.KM[lcc]);
+        uint4 bd4 = *reinterpret_cast<const uint4 *>(&sm.BD[lcc]);
         uint4 bw[NBQ], ow[NBQ];
 #pragma unroll
         for (int q = 0; q < NBQ; ++q) {
@@ -1419,35 +1520,48 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 if constexpr (OVP) ow[q] = *reinterpret_cast<const uint4 *>(&sm.OV[(4 * q + lrow + kPad) * kWave + lcc]);
             }
         }
+        // every read (keep / dirty masks, board and overlay rows) issued before
+        // anything uses one: one LDS round trip
+        // (the masks pass through an empty volatile asm placed after the row
+        // reads: their first use cannot float above those reads -- it did,
+        // splitting the batch in two round trips)
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("" : "+v"(km.x), "+v"(km.y), "+v"(km.z), "+v"(km.w), "+v"(bd4.x), "+v"(bd4.y), "+v"(bd4.z),
+                     "+v"(bd4.w));
+        const uint32_t bdl = (bd4.x | bd4.y | bd4.z | bd4.w) >> lrow;
         // the board array as one resource: byte offsets < W * stride * 4 <= 2^31
         const auto rb = buf_rsrc(p.board, (uint32_t)W * (uint32_t)sd * 4u);
         const uint32_t boff = ((uint32_t)e0 * 4u + loff * 4u);
         const bool wide_obs1 = OVP && (p.n & 3) == 0 && e0 + kWave <= p.n &&
                                (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0 &&
                                (!VEC || (reinterpret_cast<uintptr_t>(p.final_obs) & 15u) == 0);
+        // obs rows board | overlay (a reset env's terminal board included):
+        // no branch around the stores (a store on one path only made the
+        // compiler wait for every LDS read at the join) -- a null range
+        // drops them when the obs go the per-lane way below (or nowhere),
+        // and rows past W lie past the range
+        [[maybe_unused]] const auto ro = buf_rsrc(wide_obs1 ? p.obs : nullptr, (uint32_t)W * (uint32_t)p.n * 4u);
+        [[maybe_unused]] const auto rf = buf_rsrc(VEC && wide_obs1 ? p.final_obs : nullptr,
+                                                  (uint32_t)W * (uint32_t)p.n * 4u);
 #pragma unroll
         for (int q = 0; q < NBQ; ++q) {
             if (WT || 4 * q < W) {
                 uint4 v = bw[q];
-                if constexpr (OVP) {  // obs row: board | overlay (a reset env's terminal board included)
-                    if (p.obs && wide_obs1 && 4 * q + lrow < W) {
-                        const uint4 o = ow[q];
-                        const uint4 ob = make_uint4((v.x | o.x) & hmask, (v.y | o.y) & hmask, (v.z | o.z) & hmask,
-                                                    (v.w | o.w) & hmask);
-                        const uint32_t ooff =
-                            ((uint32_t)e0 + (uint32_t)(4 * q + lrow) * (uint32_t)p.n + (uint32_t)lcc) * 4u;
-                        if constexpr (VEC) {
-                            // reset envs (km = 0): the reset obs here, the
-                            // terminal one to final_obs (groups with a reset)
-                            const bool fin = p.final_obs && !(km.x && km.y && km.z && km.w);
-                            buf_store16<kNT>(buf_rsrc(p.final_obs, (uint32_t)W * (uint32_t)p.n * 4u),
-                                             fin ? ooff : kOff, ob);
-                            const uint4 keep = p.final_obs ? km : make_uint4(~0u, ~0u, ~0u, ~0u);
-                            buf_store16<kNT>(buf_rsrc(p.obs, (uint32_t)W * (uint32_t)p.n * 4u), ooff,
-                                             make_uint4(ob.x & keep.x, ob.y & keep.y, ob.z & keep.z, ob.w & keep.w));
-                        } else {
-                            buf_store16<kNT>(buf_rsrc(p.obs, (uint32_t)W * (uint32_t)p.n * 4u), ooff, ob);
-                        }
+                if constexpr (OVP) {
+                    const uint4 o = ow[q];
+                    const uint4 ob = make_uint4((v.x | o.x) & hmask, (v.y | o.y) & hmask, (v.z | o.z) & hmask,
+                                                (v.w | o.w) & hmask);
+                    const uint32_t ooff =
+                        ((uint32_t)e0 + (uint32_t)(4 * q + lrow) * (uint32_t)p.n + (uint32_t)lcc) * 4u;
+                    if constexpr (VEC) {
+                        // reset envs (km = 0): the reset obs here, the
+                        // terminal one to final_obs (groups with a reset)
+                        const bool fin = !(km.x && km.y && km.z && km.w);
+                        buf_store16<kNT>(rf, fin ? ooff : kOff, ob);
+                        const uint4 keep = p.final_obs ? km : make_uint4(~0u, ~0u, ~0u, ~0u);
+                        buf_store16<kNT>(ro, ooff, make_uint4(ob.x & keep.x, ob.y & keep.y, ob.z & keep.z, ob.w & keep.w));
+                    } else {
+                        buf_store16<kNT>(ro, ooff, ob);
                     }
                 }
                 v.x &= km.x;
@@ -1957,7 +2071,6 @@ struct RoLds {
     uint32_t cpg[kWave];  // per lane: valid << 31 | cur << 10 | pg after a chunk (output -> draw)
     uint32_t fl, fd, fo, fq;  // progress counters (see above)
 };
-
 // d[r] by selects on values (a select between two array elements would be
 // a pointer select, which puts the array in scratch memory)
 __device__ __forceinline__ uint2 sel4(const uint2 (&d)[4], int r) {
@@ -2062,8 +2175,8 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
         uint32_t tab_m = 0, tab_g = 0;
 #pragma unroll
         for (int i = 0; i < 28; ++i) {
-            asm("v_writelane_b32 %0, %1, %2" : "+v"(tab_m) : "s"(kTab.m[i]), "i"(i));
-            asm("v_writelane_b32 %0, %1, %2" : "+v"(tab_g) : "s"(kTab.g[i]), "i"(i));
+            asm("v_writelane_b32 %0, %1, %2" : "+v"(tab_m) : "s"(kBox.m[i]), "i"(i));
+            asm("v_writelane_b32 %0, %1, %2" : "+v"(tab_g) : "s"(kBox.g[i]), "i"(i));
         }
 #pragma unroll
         for (int x = 0; x < kPad; ++x) {
@@ -2109,6 +2222,12 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
 #pragma unroll
         for (int r = 0; r < 4; ++r) d4[r] = tab((int)(pw & 7u) * 4 + r);
         bool bad_act = false;
+        // LAZYH (fixed width): holes is counted when read -- a death, a holes
+        // reward, the epilogue -- not at every lock (the board changes only
+        // at locks, clears and resets, so the epilogue's count of the final
+        // board equals the count at the last lock); hstale: a lock since
+        constexpr bool LAZYH = WT != 0;
+        bool hstale = false;
         uint32_t nq = 0;  // pieces this env consumed so far (its next spawn: ring slot nq & 3)
         // The actions come from the ring the draw wave fills four steps ahead
         // (at the end of round t - 4, or its initial loads for t < 4, published
@@ -2119,24 +2238,31 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
         // starts with its action in a register: no poll, no LDS round trip.
         lds_flag_wait_ge(&sm.fd, 1u);
         uint32_t act_n = sm.act[0][lane];
+        // the piece word's fields live in registers across steps (packed only
+        // where it is published and stored)
+        int pid = (int)(pw & 7u), prot = (int)((pw >> 3) & 3u), pax = (int)((pw >> 5) & 63u),
+            pay = (int)((pw >> 11) & 63u), plock = (int)(pw >> 17);
+        // the current rotation's descriptor, carried across
+        // steps (set where the rotation or the piece changes)
+        uint2 pdesc = sel4(d4, prot);
         for (int t = 0; t < K; ++t) {
             const uint32_t act = real ? act_n : 6u;
             bad_act |= act > 6u;
-            int rot = (int)((pw >> 3) & 3u);
-            int ax = (int)((pw >> 5) & 63u);
-            int ay = (int)((pw >> 11) & 63u);
-            int lock = (int)(pw >> 17);
+            int rot = prot;
+            int ax = pax;
+            int ay = pay;
+            int lock = plock;
             stamp(1);
             // ---- action (tetris_env.py:245; value_action_map :152-160) + drop ----
             // both descriptors from registers: the columns are one LDS round trip
             const bool tries = act == 0u || act == 1u || act == 4u || act == 5u;
             const int cx = ax + (act == 0u ? -1 : (act == 1u ? 1 : 0));
-            const int cr = act == 4u ? ((rot + 1) & 3) : (act == 5u ? ((rot + 3) & 3) : rot);
-            uint2 desc = sel4(d4, rot);
+            const int cr = (rot + (act == 4u ? 1 : 0) + (act == 5u ? 3 : 0)) & 3;  // (selects: the ternary chain became an exec-mask branch)
+            uint2 desc = pdesc;
             const uint2 cdesc = sel4(d4, cr);
             uint32_t cur[4], cand[4];
-            read_cols(L, lane, desc.y, ax, cur);
-            read_cols(L, lane, cdesc.y, cx, cand);
+            read_box(L, lane, desc.y, ax, cur);
+            read_box(L, lane, cdesc.y, cx, cand);
             // the queue / planes hand-off, read optimistically in the same
             // LDS round trip as the columns: both counters, step t + 1's
             // action and the queue word; taken after the action phase if
@@ -2156,7 +2282,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             desc.y = ok ? cdesc.y : desc.y;
 #pragma unroll
             for (int j = 0; j < 4; ++j) cur[j] = ok ? cand[j] : cur[j];
-            int d = drop_v(desc.y, ay, cur);
+            int d = drop_box(desc.y, ay, cur);
             if (act == 2u) {                  // hard_drop :54-59
                 ay += d;
                 d = 0;
@@ -2175,7 +2301,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             bool locknow = false;
             if (d == 0) {
                 const int l1 = lock + 1;
-                lock = l1 < p.lock_mod ? l1 : (l1 == p.lock_mod ? 0 : l1 % p.lock_mod);
+                lock = lock_next(l1, p.lock_mod);
                 locknow = lock == 0 && !(kAblate & 1u);
             }
             stamp(2);
@@ -2216,7 +2342,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             bool died = false, spawn = false;
             [[maybe_unused]] uint32_t tb[WT ? WT : 1];  // the board after the lock (a reset copies it to OV)
             if (locknow) {
-                paint<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
+                paint_box<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
                 uint32_t andv = ~0u, orv = 0, sctz = 0, spop = 0;
                 if constexpr (WT != 0) {
                     // all column reads before any use: one LDS round trip (see
@@ -2229,8 +2355,10 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                         const uint32_t v = tb[x];
                         andv &= v;
                         orv |= v;
-                        sctz += __builtin_ctz(v);
-                        spop += __builtin_popcount(v);
+                        if constexpr (!LAZYH) {
+                            sctz += __builtin_ctz(v);
+                            spop += __builtin_popcount(v);
+                        }
                     }
                 } else {
 #pragma unroll 8
@@ -2267,8 +2395,10 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                             tb[x] = v;
                             col(L, x) = v;
                             orv |= v;
-                            sctz += __builtin_ctz(v);
-                            spop += __builtin_popcount(v);
+                            if constexpr (!LAZYH) {
+                                sctz += __builtin_ctz(v);
+                                spop += __builtin_popcount(v);
+                            }
                         }
                     } else {
 #pragma unroll 8
@@ -2283,7 +2413,20 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                     lines += ncl;
                 }
                 orv &= hmask;
-                const int32_t nh = W * H - (int32_t)sctz - ((int32_t)spop - W * (32 - H));  // _count_holes :218-220
+                // _count_holes :218-220 (LAZYH: from tb where it is needed)
+                const auto count_holes = [&]() -> int32_t {
+                    if constexpr (LAZYH) {
+                        uint32_t hc = 0, hp = 0;
+#pragma unroll
+                        for (int x = 0; x < (WT ? WT : 1); ++x) {
+                            hc += __builtin_ctz(tb[x]);
+                            hp += __builtin_popcount(tb[x]);
+                        }
+                        sctz = hc;
+                        spop = hp;
+                    }
+                    return W * H - (int32_t)sctz - ((int32_t)spop - W * (32 - H));
+                };
                 if (kFlags & ST_ADVANCED_CLEARS) {  // :266-269
                     constexpr uint64_t kClr = (40ull << 12) | (100ull << 24) | (300ull << 36) | (1200ull << 48);
                     const int32_t sc = ncl <= 4 ? (int32_t)((kClr >> (12 * ncl)) & 0xFFFu) : 0;
@@ -2297,13 +2440,18 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                     score += ncl;
                 }
                 if (orv & 1u) {  // death :277-281
-                    holes = nh;
+                    holes = count_holes();
+                    hstale = false;
                     deaths += 1;
                     died = true;
                     rew = -100;
                 } else {  // :283-299
                     const int32_t old_holes = holes;
-                    holes = nh;
+                    // holes feeds the reward only under the two holes flags;
+                    // otherwise it is recounted from the board where it is
+                    // read next (a death, the epilogue)
+                    if (!LAZYH || (kFlags & (ST_PENALISE_HOLES | ST_PENALISE_HOLES_INCREASE))) holes = count_holes();
+                    else hstale = true;
                     const int32_t hgt = __builtin_popcount(orv);
                     if (kFlags & ST_PENALISE_HEIGHT) {
                         rew -= hgt;
@@ -2341,12 +2489,14 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             // _set_piece(False), :303), the obs keeps it (overlay); a death
             // with auto-reset: the obs is the whole terminal board (overlay
             // plane), the board becomes empty (clear(), :306-315)
-            if (died && !reset_now) erase<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
+            if (died && !reset_now) erase_box<S32>(L, lane, desc.x, desc.y, ax, ay, hmask);
             const uint2 od = make_uint2(spawn ? s4[0].x : desc.x, spawn ? s4[0].y : desc.y);
             const int oax = spawn ? W / 2 : ax, oay = spawn ? 0 : ay;
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                OV[(oax + pc_dx(od.y, j) + kPad) * kWave + lane] = pc_bits<S32>(od.x, j, oay) & hmask;
+            for (int j = 0; j < 4; ++j) {
+                const int ox = box_x0(od.y, oax) + j;
+                OV[(ox + kPad) * kWave + lane] = pc_bits<S32>(od.x, j, oay) & hmask;
+            }
             if (reset_now) {
                 if constexpr (WT != 0) {
 #pragma unroll
@@ -2369,10 +2519,17 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 sm.ep[t & 1][2][lane] = (uint32_t)lines;
                 sm.ep[t & 1][3][lane] = (uint32_t)holes;
                 time = score = lines = holes = height = 0;
+                hstale = false;
             }
-            if (lane == 0) lds_flag_set(&sm.fo, (uint32_t)t + 1u);
             // ---- state for the next step ----
-            pw = pack_piece(draw ? sid : (int)(pw & 7u), draw ? 0 : rot, draw ? W / 2 : ax, draw ? 0 : ay, lock);
+            pid = draw ? sid : pid;
+            prot = draw ? 0 : rot;
+            pax = draw ? W / 2 : ax;
+            pay = draw ? 0 : ay;
+            plock = lock;
+            pdesc.x = draw ? s4[0].x : desc.x;
+            pdesc.y = draw ? s4[0].y : desc.y;
+            if (lane == 0) lds_flag_set(&sm.fo, (uint32_t)t + 1u);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 d4[r].x = draw ? s4[r].x : d4[r].x;
@@ -2386,10 +2543,22 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
         ss(ST_STAT_TIME) = (uint32_t)time;
         ss(ST_STAT_SCORE) = (uint32_t)score;
         ss(ST_STAT_LINES) = (uint32_t)lines;
+        if constexpr (LAZYH) {
+            if (hstale) {
+                uint32_t hc = 0, hp = 0;
+#pragma unroll
+                for (int x = 0; x < (WT ? WT : 1); ++x) {
+                    const uint32_t v = col(L, x);
+                    hc += __builtin_ctz(v);
+                    hp += __builtin_popcount(v);
+                }
+                holes = W * H - (int32_t)hc - ((int32_t)hp - W * (32 - H));
+            }
+        }
         ss(ST_STAT_HOLES) = (uint32_t)holes;
         ss(ST_STAT_PIECE_HEIGHT) = (uint32_t)height;
         ss(ST_STAT_DEATHS) = (uint32_t)deaths;
-        ss(kPieceRow) = pw;
+        ss(kPieceRow) = pack_piece(pid, prot, pax, pay, plock);
         wave_sync();
         const auto rb = buf_rsrc(p.board, (uint32_t)((W + 3) & ~3) * (uint32_t)sd * 4u);
         const uint32_t boff = (uint32_t)e0 * 4u + loff * 4u;

@@ -687,15 +687,20 @@ def test_async_action_check():
     b.close()
 
 
+@pytest.mark.parametrize("scoring", ["penalties", "default"])
 @pytest.mark.parametrize("autoreset", ["same_step", "none"])
 @pytest.mark.parametrize("board", [(10, 20), (9, 15)])
-def test_rollout_equals_steps(autoreset, board):
-    """st_rollout(K) == K x st_step, bit-exact, outputs and final state."""
+def test_rollout_equals_steps(autoreset, board, scoring):
+    """st_rollout(K) == K x st_step, bit-exact, outputs and final state.
+    "default" scoring (no holes term in the reward): the rollout counts holes
+    only where it reads them (a death, the final state), st_step at every
+    lock -- the final holes counters and the episode counters must agree."""
     G = _engine()
     W, H = board
     n, K = 1000, 150
-    kw = dict(width=W, height=H, lock_delay=1, step_reset=True, penalise_holes_increase=True,
-              advanced_clears=True, penalise_height_increase=True)
+    kw = dict(width=W, height=H, lock_delay=1, step_reset=True)
+    if scoring == "penalties":
+        kw.update(penalise_holes_increase=True, advanced_clears=True, penalise_height_increase=True)
     a = G.TetrisBatch(n, autoreset=autoreset, seeds=[3 + e for e in range(n)], **kw)
     b = G.TetrisBatch(n, autoreset=autoreset, seeds=[3 + e for e in range(n)], **kw)
     a.reset()
