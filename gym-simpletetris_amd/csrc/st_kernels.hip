@@ -326,6 +326,13 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     y ^= (y >> 18);
     return y;
 }
+// The tempering without its last step (y ^= y >> 18), which changes bits < 14
+// only: the top 18 bits of the result are exact.
+__device__ __forceinline__ uint32_t mt_temper_hi18(uint32_t y) {
+    y ^= (y >> 11);
+    y = __builtin_amdgcn_bitop3_b32(y, y << 7, 0x9d2c5680u, 0x78);
+    return __builtin_amdgcn_bitop3_b32(y, y << 15, 0xefc60000u, 0x78);
+}
 __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
     const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
     return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
@@ -781,16 +788,28 @@ __device__ __forceinline__ int draw_win(bool need, const int32_t (&cnt)[7], uint
         const int nv = o < 8 ? wlim - o : 0;  // valid words from o
         // words 0-3 tempered as independent chains (acceptance >= 1/2, ~0.7
         // typically: 4 rejections in a row are rare), 4-7 where a lane needs them
+        // getrandbits(kb) = the top kb bits: with kb <= 18 on every lane
+        // (n < 2^18: any counts the game itself produces) the tempering's
+        // last step is skipped (mt_temper_hi18), and y >> (32 - kb) < n is
+        // tested as y < n << (32 - kb), one shift for the accepted word
+        const bool tail = __ballot(kb > 18) != 0;
+        const uint32_t ns = n << (32 - kb);
         auto pass = [&](int j0) {
             int first = 4;
             uint32_t rr = 0;
+            auto words = [&](auto tl) {
 #pragma unroll
-            for (int j = 3; j >= 0; --j) {
-                const uint32_t y = mt_temper(w8[j0 + j]) >> (32 - kb);
-                const bool acc = y < n && j0 + j < nv;
-                first = acc ? j : first;
-                rr = acc ? y : rr;
-            }
+                for (int j = 3; j >= 0; --j) {
+                    uint32_t y = mt_temper_hi18(w8[j0 + j]);
+                    if constexpr (decltype(tl)::value) y ^= y >> 18;
+                    const bool acc = y < ns && j0 + j < nv;
+                    first = acc ? j : first;
+                    rr = acc ? y : rr;
+                }
+            };
+            if (tail) words(std::true_type{});
+            else words(std::false_type{});
+            rr >>= (32 - kb);
             if (pending) {
                 int pos;
                 if (first < 4) {
@@ -2673,18 +2692,21 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             const bool cons = real && ((w >> (lane & 31)) & 1u) && !(kAblate & 2u);
             // step s consumed q0: count it (_new_piece :199), commit q1 as the
             // preview, draw the piece after it
-            // (cq = cnt_r + the head's count is kept across rounds: a spawn
-            // makes cnt_r = cq, and the new head q1 adds its own)
-#pragma unroll
-            for (int i = 0; i < 7; ++i) cnt_r[i] = cons ? cq[i] : cnt_r[i];
+            // (cq = the spawned pieces' counts + the head's, kept across
+            // rounds: a spawn adds the new head q1's; the spawned counts
+            // alone are derived once, at the end)
             if (cons) {
                 mtc = pv_pack(mta, q1, c1);
                 q0 = q1;
             }
+            {
+                const uint32_t oh = cons ? 1u << q0 : 0u;  // one bfe + add per shape
 #pragma unroll
-            for (int i = 0; i < 7; ++i) cq[i] += (cons && i == q0);
+                for (int i = 0; i < 7; ++i) cq[i] += (int32_t)((oh >> i) & 1u);
+            }
             const uint32_t m0 = mta;
             const int pk = draw_win<CHO>(cons, cq, mta, win, o, wlim, mtg, sm.S, lane);
+            stamp(5);
             if (cons) {
                 q1 = pk;
                 c1 = mt_consumed(m0, mta);
@@ -2716,7 +2738,9 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             // windows: merge the reload of the previous round, reload where
             // this round drew (valid words by the progress before this
             // round's chunk: conservative)
+            stamp(6);
             mt_win_consume<kMtWin>(wn);
+            stamp(7);
             if (rl) {
 #pragma unroll
                 for (int j = 0; j < kMtWin; ++j) win.w[j] = wn.w[j];
@@ -2754,7 +2778,9 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             mtc = mt_keep(mtc, mt_pack(ic, cc == ca ? pga : kMtN, cc));
         }
 #pragma unroll
-        for (int i = 0; i < 7; ++i) ss(ST_STAT_COUNT0 + i) = (uint32_t)cnt_r[i];
+        // the spawned pieces' counts = cq less the queue head's, which cq
+        // already holds (cq = cnt_r + the head's count throughout the loop)
+        for (int i = 0; i < 7; ++i) ss(ST_STAT_COUNT0 + i) = (uint32_t)(cq[i] - (i == q0 ? 1 : 0));
         ss(ST_STAT_MT_INDEX) = mtc;
         wave_sync();
     } else {

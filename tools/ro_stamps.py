@@ -31,8 +31,8 @@ out = {}
 # phases in execution order, by the stamp index that ends them
 LOGIC = [(1, "step start (action load)"), (2, "action + drop"), (3, "queue / planes wait"),
          (4, "lock path"), (5, "reward/done + mask"), (6, "obs planes + state")]
-DRAW = [(1, "round start"), (2, "chunk issue + mask wait"), (3, "draw + ring"),
-        (4, "chunk store + windows")]
+DRAW = [(1, "round start"), (2, "chunk issue + mask wait"), (5, "draw"), (3, "ring + publish"),
+        (6, "chunk bookkeeping"), (7, "window reload wait"), (4, "merge + reload issue")]
 OUT = [(1, "wait for the planes"), (2, "obs stores + clear")]
 res = []
 for c in range(NL):
