@@ -1239,3 +1239,53 @@ def test_host_written_lock_fields(lock_delay, step_reset):
         assert np.array_equal(d.cpu().numpy().astype(np.uint8), ref["done"][t]), t
         assert np.array_equal(o.cpu().numpy().view(np.uint32).T, ref["obs"][t]), t
         assert torch.equal(ro[t], o) and torch.equal(rr[t], r) and torch.equal(rd[t], d), t
+
+
+@pytest.mark.parametrize("mode", ["step", "rollout"])
+def test_host_written_large_shape_counts(mode):
+    """Shape counts a host wrote far apart (st_set_state): randint's range n =
+    35 + 7 max - sum reaches 2^18..2^25, so getrandbits takes 19-25 bits
+    (tetris_env.py:183-191; Lib/random.py _randbelow).  The rollout's draw
+    skips the tempering's last step only in waves whose lanes all draw <= 18
+    bits: one wave here has none of the wide lanes, one only wide lanes, two
+    a mix.  Outputs and final counts / MT index vs the oracle."""
+    G = _engine()
+    n, T = 256, 80
+    b = G.TetrisBatch(n, autoreset="same_step", seeds=range(n))
+    b.reset()
+    ob = O.OracleBatch(n, list(range(n)))
+    ob.reset()
+    st = b.get_state(("mt", "stats"))  # st_mt_sync: no preview drawn with the old counts
+    mt, stats = st["mt"].copy(), st["stats"].copy()
+    rng = np.random.default_rng(23)
+    for i in range(n):
+        if 64 <= i < 128:
+            counts = np.array([100_000 + 1_000 * i, 0, 0, 0, 0, 0, 0])
+        elif i >= 128 and i % 2:
+            counts = rng.integers(0, 3_000_000, 7)
+        else:
+            counts = stats[6:13, i].astype(np.int64)
+        stats[6:13, i] = counts
+        e = ob.envs[i]
+        for k in range(624):
+            e.rng.mt[k] = int(mt[i, k])
+        e.rng.index = int(stats[13, i])
+        ob.set_state(i, counts=counts)
+    b.set_state(mt=mt, stats=stats)
+    acts = O.splitmix64_actions(9, 0, T, n)
+    acts[1::2] = 2  # hard drops: a lock at least every other step
+    ref = ob.rollout(acts)
+    if mode == "step":
+        for t in range(T):
+            obs, rew, done = b.step(torch.as_tensor(acts[t], device=b.device))
+            assert np.array_equal(rew.cpu().numpy(), ref["reward"][t]), t
+            assert np.array_equal(obs.cpu().numpy().view(np.uint32).T, ref["obs"][t]), t
+    else:
+        obs, rew, done = b.rollout(torch.as_tensor(acts, device=b.device))
+        assert np.array_equal(rew.cpu().numpy(), ref["reward"])
+        assert np.array_equal(done.cpu().numpy().astype(np.uint8), ref["done"])
+        assert np.array_equal(obs.cpu().numpy().view(np.uint32).transpose(0, 2, 1), ref["obs"])
+    fin = b.get_state(("mt", "stats"))
+    for i in range(n):
+        assert list(fin["stats"][6:13, i].astype(np.int64)) == list(np.ctypeslib.as_array(ob.envs[i].counts)), i
+        assert int(fin["stats"][13, i]) == ob.envs[i].rng.index, i
