@@ -16,10 +16,12 @@ processes itself (before anything touches a GPU) with the rendezvous on
 127.0.0.1; under torch.distributed.run it is one of the ranks.  Each rank owns
 a contiguous block of global env indices (seeds and actions keyed by the
 global index, so the work is identical at any N; "scaling": "weak"), and each
-timed step is BASELINE config C5's step: st_step on every shard, then the
+timed step is BASELINE config C5's step: st_step_wire on every shard, the
 RCCL gather of every shard's packed obs/reward/done to rank 0, double-buffered
-(step t+1 computes into the other buffer while the gather of step t runs).
-The same steps without the gather are reported beside it (`step_no_gather`).
+(step t+1 computes into the other buffer while the gather of step t runs), and
+rank 0's decode of the gathered rows into the global obs / reward / done
+(st_unwire_shards).  The same steps without the decode (`gather.no_decode`)
+and without the gather (`step_no_gather`) are reported beside it.
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -511,8 +513,23 @@ def main():
                 self.gfn = self.fn
                 views = [[ctypes.c_void_p(v.data_ptr()) for v in buffer_views(b, W)] for b in self.gbufs]
             rdev = dev if self.nccl else torch.device("cpu")  # gloo gathers host tensors
-            self.grecv = [[torch.empty(b.shape, dtype=b.dtype, device=rdev) for _ in range(world)]
-                          if rank == 0 else None for b in self.gbufs]
+            # rank 0 receives each step into one contiguous [world][rows][n]
+            # buffer (per step parity), gathered into its views
+            self.grecv_buf = [torch.empty((world,) + tuple(b.shape), dtype=b.dtype, device=rdev)
+                              if rank == 0 else None for b in self.gbufs]
+            self.grecv = [list(rb.unbind(0)) if rb is not None else None for rb in self.grecv_buf]
+            # rank 0's decoded global outputs of every step (wire: st_unwire_shards
+            # of the receive buffer, inside the timed region): obs [W][N], reward, done
+            if rank == 0 and self.wire:
+                self.gout = (torch.empty((W, self.n_global), dtype=torch.int32, device=dev),
+                             torch.empty(self.n_global, dtype=torch.int32, device=dev),
+                             torch.empty(self.n_global, dtype=torch.bool, device=dev))
+                self.gdec = (ctypes.c_void_p(self.gout[0].data_ptr()), ctypes.c_void_p(self.gout[1].data_ptr()),
+                             ctypes.c_void_p(self.gout[2].data_ptr()))
+                self.grecv_dev = [rb if self.nccl else torch.empty(rb.shape, dtype=rb.dtype, device=dev)
+                                  for rb in self.grecv_buf]
+            self.decode = True
+            self.ndecodes = 0
             ctx = self.eng._ctx
             if self.wire:
                 self.gargs = [(ctx, self.aptr[t], ctypes.c_void_p(self.gbufs[t & 1].data_ptr()), sp)
@@ -525,66 +542,111 @@ def main():
             self.gworks = [None, None]
             self.ngathers = 0
 
+        def decode_step(self, k):
+            """Rank 0, wire format: st_unwire_shards of step parity k's
+            receive buffer into the global obs / reward / done (on s, after
+            the gather that filled it: its work was waited on s)."""
+            src = self.grecv_dev[k]
+            if not self.nccl:  # gloo: the host receive buffer to the GPU first
+                src.copy_(self.grecv_buf[k], non_blocking=False)
+            rc = self.eng._L.st_unwire_shards(W, H, self.n_global, world, self.n_local, ctypes.c_void_p(src.data_ptr()),
+                                   *self.gdec, sp)
+            self.ndecodes += 1
+            return rc
+
         def gather_range(self, t0, t1):
             """Steps t0 .. t1-1, each one st_step into buffer t % 2 and one
             gather of that buffer to rank 0.  With RCCL the gather runs on
             the collective's stream after the step (ProcessGroupNCCL orders
             it behind the current stream, s), so step t+1 overlaps the gather
             of step t; before step t+2 reuses a buffer, s waits for the gather
-            that read it.  All gathers are complete on s when this returns."""
+            that read it.  With the wire format and self.decode, rank 0
+            decodes every step's gathered outputs into the global obs /
+            reward / done (BASELINE C5's deliverable) one step later: after
+            step t+1 is enqueued, s waits for the gather of step t and runs
+            st_unwire_shards on it, so the gather of step t still overlaps
+            step t+1.  All gathers (and decodes) are complete on s when this
+            returns."""
             fn, rc = self.gfn, 0
+            dec = self.decode and self.wire and rank == 0
+            pend = None  # step parity whose gather rank 0 has yet to decode
             for t in range(t0, t1):
                 k = t & 1
                 if self.gworks[k] is not None:
                     self.gworks[k].wait()  # s (not the host) waits for the gather of step t - 2
+                    self.gworks[k] = None
                 rc = rc or fn(*self.gargs[t])
+                if dec and pend is not None:
+                    if self.gworks[pend] is not None:
+                        self.gworks[pend].wait()  # s waits for the gather of step t - 1
+                        self.gworks[pend] = None
+                    rc = rc or self.decode_step(pend)
+                    pend = None
                 if self.nccl:
                     self.gworks[k] = dist.gather(self.gbufs[k], gather_list=self.grecv[k], dst=0, async_op=True)
                 else:  # gloo: through host memory, no overlap
                     s.synchronize()
                     dist.gather(self.gbufs[k].cpu(), gather_list=self.grecv[k], dst=0)
                 self.ngathers += 1
+                pend = k
             for k in (0, 1):
                 if self.gworks[k] is not None:
                     self.gworks[k].wait()
                     self.gworks[k] = None
+            if dec and pend is not None:
+                rc = rc or self.decode_step(pend)
             C.check(rc)
 
         def measure_gather(self):
-            """C5's timed region: K x (st_step + gather to rank 0) after WU
-            such steps untimed.  Rank 0's assembled outputs of the last timed
-            step go to $ST_BENCH_DUMP (an .npz) when set (tests compare them
-            with the oracle)."""
+            """C5's timed region: K x (st_step + gather to rank 0 + rank 0's
+            decode of the gathered wire rows into the global obs / reward /
+            done) after WU such steps untimed; then the same K steps without
+            the decode, reported beside (`no_decode`).  Rank 0's decoded
+            outputs of the last timed step go to $ST_BENCH_DUMP (an .npz)
+            when set (tests compare them with the oracle)."""
             self.setup_gather()
             with torch.cuda.stream(s):
                 self.gather_range(0, WU)
             torch.cuda.synchronize(dev)
-            g0 = self.ngathers
+            g0, d0 = self.ngathers, self.ndecodes
             el, ev_ms, p_lock = timed(self.eng, lambda: self.gather_range(WU, WU + K), K)
-            ng = self.ngathers - g0
+            ng, nd = self.ngathers - g0, self.ndecodes - d0
             dump = os.environ.get("ST_BENCH_DUMP")
             if rank == 0 and dump:
                 import numpy as np
-                from gym_simpletetris_amd.distributed import assemble, assemble_wire
-                got = self.grecv[(WU + K - 1) & 1]
-                if self.wire:  # rank 0 unpacks the gathered rows (st_unwire), outside the region
-                    o, r, d = (x.cpu() for x in assemble_wire(got, W, H))
+                from gym_simpletetris_amd.distributed import assemble
+                if self.wire:  # the region's own last decode (st_unwire_shards)
+                    torch.cuda.synchronize(dev)
+                    o, r, d = (x.cpu() for x in self.gout)
                 else:
+                    got = self.grecv[(WU + K - 1) & 1]
                     o, r, d = assemble([b.cpu() for b in got], W)
                 np.savez(dump, obs=o.numpy().view(np.uint32), reward=r.numpy(), done=d.numpy(),
-                         step=WU + K - 1, n_global=self.n_global, gathers_timed=ng)
+                         step=WU + K - 1, n_global=self.n_global, gathers_timed=ng, decodes_timed=nd)
             bpr = self.gbufs[0].numel() * 4
             ms = el / K * 1e3
-            return {"value": self.n_global * K / el, "ms_per_step": ms, "event_ms_per_step": ev_ms / K,
-                    "p_lock": p_lock, "gathers_timed": ng,
-                    "gather": {"backend": args.backend, "collective": "torch.distributed.gather to rank 0",
-                               "format": ("st_step_wire: %d words per env (obs bits, reward low 16, done)"
-                                          % self.eng.wire_words if self.wire else
-                                          "st_step rows: packed obs [W] + reward + done per env"),
-                               "gathers_in_timed_region": ng, "bytes_per_rank_per_step": bpr,
-                               "bytes_into_rank0_per_step": bpr * (world - 1),
-                               "rank0_ingress_GBps": bpr * (world - 1) / (ms * 1e-3) / 1e9,
-                               "overlap": "double-buffered: step t+1 computes while step t is gathered"}}
+            out = {"value": self.n_global * K / el, "ms_per_step": ms, "event_ms_per_step": ev_ms / K,
+                   "p_lock": p_lock, "gathers_timed": ng,
+                   "gather": {"backend": args.backend, "collective": "torch.distributed.gather to rank 0",
+                              "format": ("st_step_wire: %d words per env (obs bits, reward 32 bits, done)"
+                                         % self.eng.wire_words if self.wire else
+                                         "st_step rows: packed obs [W] + reward + done per env"),
+                              "gathers_in_timed_region": ng, "decodes_in_timed_region_rank0": nd,
+                              "decode": ("rank 0: st_unwire_shards of each step's receive buffer into the "
+                                         "global obs [W][N] / reward / done, on the step stream, inside the "
+                                         "region" if self.wire else "none (the rows are st_step's outputs)"),
+                              "bytes_per_rank_per_step": bpr,
+                              "bytes_into_rank0_per_step": bpr * (world - 1),
+                              "rank0_ingress_GBps": bpr * (world - 1) / (ms * 1e-3) / 1e9,
+                              "overlap": "double-buffered: step t+1 computes while step t is gathered"}}
+            if self.wire:
+                self.decode = False
+                el2, ev2, _ = timed(self.eng, lambda: self.gather_range(WU, WU + K), K)
+                self.decode = True
+                out["no_decode"] = {"value": self.n_global * K / el2, "ms_per_step": el2 / K * 1e3,
+                                    "event_ms_per_step": ev2 / K,
+                                    "basis": "the same K steps + gathers again, rank 0 not decoding"}
+            return out
 
         def runner(self):
             if args.launch == "eager":
@@ -609,11 +671,57 @@ def main():
             el, ev_ms, p_lock = timed(self.eng, run, S)
             return ev_ms * 1e3 / S, p_lock
 
+        def region_probe(self):
+            """Debug record of the timed region's shape (outside `value`): the
+            same K eager launches run twice more right after the region, from
+            the same idle-GPU start (barrier + synchronize): (1) with a host
+            perf_counter stamp after every launch call and HIP events only
+            around the region -- the host's submission timeline, unperturbed;
+            (2) with a HIP event recorded before every launch -- each launch's
+            GPU span (the events add host time per launch, so the host falls
+            behind the GPU sooner than in the region: read its shape, not its
+            sum)."""
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(K + 1)]
+            fn, args_ = self.fn, self.args[WU:WU + K]
+            out = {}
+            with torch.cuda.stream(s):
+                for e in evs:  # first records are slow: not inside a probe
+                    e.record(s)
+                sync_all()
+                ev0.record(s)
+                t0 = time.perf_counter()
+                hs = []
+                for a in args_:
+                    fn(*a)
+                    hs.append(time.perf_counter())
+                ev1.record(s)
+                sync_all()
+                t1 = time.perf_counter()
+                out["host_submit_us"] = [round((h - t0) * 1e6, 2) for h in hs]
+                out["host_call_us"] = [round((b_ - a_) * 1e6, 2) for a_, b_ in zip([t0] + hs[:-1], hs)]
+                out["wall_us"] = round((t1 - t0) * 1e6, 1)
+                out["event_span_us"] = round(ev0.elapsed_time(ev1) * 1e3, 2)
+                out["sync_after_last_submit_us"] = round((t1 - hs[-1]) * 1e6, 1)
+                sync_all()
+                t0 = time.perf_counter()
+                for i, a in enumerate(args_):
+                    evs[i].record(s)
+                    fn(*a)
+                evs[K].record(s)
+                sync_all()
+                t1 = time.perf_counter()
+                out["per_launch_event_us"] = [round(evs[i].elapsed_time(evs[i + 1]) * 1e3, 2) for i in range(K)]
+                out["events_wall_us"] = round((t1 - t0) * 1e6, 1)
+            out["basis"] = ("the timed region's K launches repeated twice after it (same actions, later "
+                            "state): host stamps only, then an event before every launch; debug, not value")
+            return out
+
         def measure(self, steady=True):
             self.warmup()
             run, keep = self.runner()
             el, ev_ms, p_lock = timed(self.eng, run, K)
             del keep
+            probe = self.region_probe() if (steady and K <= 200 and args.launch == "eager") else None
             ev_us = ev_ms * 1e3 / K
             kname = kname_of("step", self.f32, self.sc0)
             bytes_at = lambda pl: s8d_bytes(pl, self.f32)  # noqa: E731
@@ -632,8 +740,11 @@ def main():
                                 "frac": s8d_bytes(st_pl, self.f32) * self.n_local / (st_us * 1e3) / HBM_PEAK_GBS,
                                 "basis": "1,000 further launches back to back after the timed region, "
                                          "HIP events around them (no region ramp / final synchronize)"}
-            return {"value": self.n_global * K / el, "ms_per_step": el / K * 1e3,
-                    "event_ms_per_step": ev_ms / K, "p_lock": p_lock, "roofline": rl}
+            r = {"value": self.n_global * K / el, "ms_per_step": el / K * 1e3,
+                 "event_ms_per_step": ev_ms / K, "p_lock": p_lock, "roofline": rl}
+            if probe is not None:
+                r["region_probe"] = probe
+            return r
 
         def close(self):
             self.eng.close()
@@ -687,6 +798,8 @@ def main():
         "event_ms_per_step": hm["event_ms_per_step"],
         "roofline": hm["roofline"],
     }
+    if "region_probe" in hm:
+        out["debug"] = {"region_probe": hm["region_probe"]}
     if use_dist:
         out["gather"] = hm["gather"]
         out["config"]["gathers_per_step"] = 1
@@ -798,12 +911,13 @@ def vec_env_variant(n: int, steps: int, dev):
     calls it: wall time per step, packed and float32 obs, without the action
     check, with the step kernel's own check ('async', the default: a sticky
     flag in mapped host memory, st_set_action_flag; no extra launch, no sync)
-    and with the per-step device->host check (True)."""
+    and with the per-step device->host check (True); copy=True (default)
+    and, with 'async', copy=False."""
     from gym_simpletetris_amd.envs.tetris_env import TetrisVecEnv
     out = {}
     for fmt in ("packed", "f32"):
-        for val in (False, "async", True):
-            v = TetrisVecEnv(n, seed=1000, obs_format=fmt, validate_actions=val, device=dev)
+        for val, cp in ((False, True), ("async", True), (True, True), ("async", False)):
+            v = TetrisVecEnv(n, seed=1000, obs_format=fmt, validate_actions=val, device=dev, copy=cp)
             v.reset()
             acts = torch.randint(0, 7, (64, n), dtype=torch.uint8, device=dev)
             for t in range(50):
@@ -814,9 +928,12 @@ def vec_env_variant(n: int, steps: int, dev):
                 v.step(acts[t % 64])
             torch.cuda.synchronize(dev)
             dt = (time.perf_counter() - t0) / steps
-            out[f"{fmt}/validate_actions={val}"] = {"us_per_step": dt * 1e6, "env_steps_per_s": n / dt}
+            key = f"{fmt}/validate_actions={val}" + ("" if cp else "/copy=False")
+            out[key] = {"us_per_step": dt * 1e6, "env_steps_per_s": n / dt}
             v.close()
-    out["note"] = ("TetrisVecEnv.step incl. the per-step info snapshot; host-bound above the kernel "
+    out["note"] = ("TetrisVecEnv.step incl. the per-step info snapshot; copy=True (the default): every "
+                   "step's outputs in tensors allocated for it (the caller's to keep); copy=False: two "
+                   "alternating output slots (overwritten two steps later); host-bound above the kernel "
                    "(DESIGN.md §5.1)")
     return out
 

@@ -220,6 +220,9 @@ int st_step_f32(st_ctx *c, const uint8_t *d_actions, uint32_t *d_obs, float *d_o
 
 int st_step_vec(st_ctx *c, const uint8_t *d_actions, uint32_t *d_obs, float *d_obs_f32, int32_t *d_reward,
                 uint8_t *d_done, uint32_t *d_final_obs, int32_t *d_info, st_stream stream) {
+    // final_obs is part of the obs output: without d_obs the kernel's two store
+    // paths would disagree on whether it is written
+    if (d_final_obs && !d_obs) return fail(ST_EINVAL, "st_step_vec: d_final_obs needs d_obs");
     return step_impl(c, d_actions, d_obs, d_obs_f32, d_reward, d_done, stream, d_final_obs, d_info);
 }
 
@@ -227,7 +230,7 @@ int st_wire_words(int32_t width, int32_t height) {
     if (width < 1 || height < 1 || width > st::kMaxW || height > st::kMaxH)
         return fail(ST_EINVAL, "st_wire_words: board %dx%d outside 1..%d x 1..%d", width, height, st::kMaxW,
                     st::kMaxH);
-    return (width * height + 17 + 31) / 32;
+    return (width * height + 33 + 31) / 32;
 }
 
 int st_step_wire(st_ctx *c, const uint8_t *d_actions, uint32_t *d_wire, st_stream stream) {
@@ -247,7 +250,21 @@ int st_unwire(int32_t width, int32_t height, int64_t n, const uint32_t *d_wire, 
     if (st_wire_words(width, height) < 0) return ST_EINVAL;
     if (n < 0) return fail(ST_EINVAL, "st_unwire: negative size");
     if (n > 0 && (!d_wire || !d_obs || !d_reward || !d_done)) return fail(ST_EINVAL, "st_unwire: null argument");
-    ST_HIP(st::launch_unwire(width, height, n, d_wire, d_obs, d_reward, d_done, (hipStream_t)stream));
+    ST_HIP(st::launch_unwire(width, height, n, 1, n, d_wire, d_obs, d_reward, d_done, (hipStream_t)stream));
+    return ST_OK;
+}
+
+int st_unwire_shards(int32_t width, int32_t height, int64_t n_global, int32_t shards, int64_t n_cap,
+                     const uint32_t *d_wire, uint32_t *d_obs, int32_t *d_reward, uint8_t *d_done, st_stream stream) {
+    if (st_wire_words(width, height) < 0) return ST_EINVAL;
+    if (n_global < 0 || shards < 1) return fail(ST_EINVAL, "st_unwire_shards: n_global < 0 or shards < 1");
+    if (n_cap < (n_global + shards - 1) / shards)
+        return fail(ST_EINVAL, "st_unwire_shards: n_cap %lld below the largest shard (%lld)", (long long)n_cap,
+                    (long long)((n_global + shards - 1) / shards));
+    if (n_global > 0 && (!d_wire || !d_obs || !d_reward || !d_done))
+        return fail(ST_EINVAL, "st_unwire_shards: null argument");
+    ST_HIP(st::launch_unwire(width, height, n_global, shards, n_cap, d_wire, d_obs, d_reward, d_done,
+                             (hipStream_t)stream));
     return ST_OK;
 }
 
@@ -347,13 +364,16 @@ int st_state(st_ctx *c, st_state_views *out) {
 namespace {
 struct SnapHeader {  // st_save / st_load, 64 bytes
     char magic[8];
-    uint32_t abi;
+    uint32_t abi;  // the snapshot format version (kSnapVersion)
     int32_t width, height, nstat;
     int64_t n;
     uint8_t pad[32];
 };
 static_assert(sizeof(SnapHeader) == 64, "snapshot header");
 const char kSnapMagic[8] = {'S', 'T', 'S', 'N', 'A', 'P', 0, 1};
+// the snapshot format's own version (written where ABI 1 wrote its ABI
+// version, 1): independent of ST_ABI_VERSION, which changes with the calls
+constexpr uint32_t kSnapVersion = 1;
 
 int64_t snap_bytes(const st_ctx *c) {
     return (int64_t)sizeof(SnapHeader) +
@@ -371,7 +391,7 @@ int st_save(st_ctx *c, void *host_out, int64_t bytes) {
     DeviceGuard g(c->device);
     SnapHeader h{};
     memcpy(h.magic, kSnapMagic, sizeof(h.magic));
-    h.abi = ST_ABI_VERSION;
+    h.abi = kSnapVersion;
     h.width = c->cfg.width;
     h.height = c->cfg.height;
     h.nstat = ST_NSTAT;
@@ -400,9 +420,9 @@ int st_load(st_ctx *c, const void *host_in, int64_t bytes) {
     SnapHeader h;
     memcpy(&h, host_in, sizeof(h));
     if (memcmp(h.magic, kSnapMagic, sizeof(h.magic)) != 0) return fail(ST_EINVAL, "st_load: not a snapshot");
-    if (h.abi != ST_ABI_VERSION || h.nstat != ST_NSTAT)
-        return fail(ST_EINVAL, "st_load: snapshot of ABI %u (%d counter rows), this is %d (%d)", h.abi,
-                    h.nstat, ST_ABI_VERSION, ST_NSTAT);
+    if (h.abi != kSnapVersion || h.nstat != ST_NSTAT)
+        return fail(ST_EINVAL, "st_load: snapshot format %u (%d counter rows), this is %u (%d)", h.abi,
+                    h.nstat, kSnapVersion, ST_NSTAT);
     if (h.width != c->cfg.width || h.height != c->cfg.height || h.n != c->n)
         return fail(ST_EINVAL, "st_load: snapshot of %lld %dx%d envs, context has %lld %dx%d",
                     (long long)h.n, h.width, h.height, (long long)c->n, c->cfg.width, c->cfg.height);

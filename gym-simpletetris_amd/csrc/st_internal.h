@@ -36,7 +36,10 @@ struct KParams {
                         // -DST_ABLATION=1 builds, tools/ablate.sh); 0 in
                         // every correct run: 1 = no lock path, 2 = no MT draw,
                         // 4 = no twist, 8 = no obs output; st_step: 1024 =
-                        // counter rows read from the first workgroup's lines
+                        // counter rows read from the first workgroup's lines,
+                        // 2048 = lock-path counter stores dropped, 4096 = board
+                        // stores dropped, 8192 = late counter loads from the
+                        // first workgroup's lines
     uint64_t *stamps;   // DIAGNOSTIC build only (env ST_STAMPS at st_create): per-wave
                         // s_memtime at 8 phase boundaries of the step kernel
     int32_t k;          // st_rollout: number of steps
@@ -75,8 +78,8 @@ hipError_t launch_policy_greedy(const KParams &p, uint64_t seed, int64_t t, uint
                                 uint8_t *out, hipStream_t s);
 hipError_t launch_grayscale(const KParams &p, const uint32_t *obs, int size, int channels,
                             int as_u8, void *out, hipStream_t s);
-hipError_t launch_unwire(int W, int H, int64_t n, const uint32_t *wire, uint32_t *obs, int32_t *reward,
-                         uint8_t *done, hipStream_t s);
+hipError_t launch_unwire(int W, int H, int64_t n_global, int shards, int64_t n_cap, const uint32_t *wire,
+                         uint32_t *obs, int32_t *reward, uint8_t *done, hipStream_t s);
 hipError_t launch_check_actions(const uint8_t *a, int64_t n, uint32_t *flag, hipStream_t s);
 hipError_t launch_gen_actions(uint8_t *out, int64_t n, int64_t t, uint64_t seed, int64_t off,
                               hipStream_t s);

@@ -856,12 +856,13 @@ __device__ __forceinline__ int win_lim(uint32_t m) {
 }
 
 // (x + 1) % lock_mod for l1 = x + 1 >= 1 (tetris_env.py:175): l1 <= lock_mod
-// except after a host-written state (a lock field up to 2^15), which the loop
-// reduces; it exits at once for every other lane.  (As a plain % the
-// division ran, exec-masked, on every step.)
+// except after a host-written state (a lock field up to 2^15), which a
+// division reduces -- only in a wave where some lane needs it (wave-uniform
+// branch: a bounded cost once per host write, not a subtraction loop of up to
+// 2^15 rounds; as a plain % the division ran, exec-masked, on every step)
 __device__ __forceinline__ int lock_next(int l1, int lock_mod) {
     int r = l1 < lock_mod ? l1 : l1 - lock_mod;
-    while (r >= lock_mod) r -= lock_mod;
+    if (__ballot(r >= lock_mod)) r = r >= lock_mod ? r % lock_mod : r;
     return r;
 }
 __device__ __forceinline__ uint32_t pack_piece(int id, int rot, int ax, int ay, int lock) {
@@ -1280,7 +1281,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     [[maybe_unused]] uint32_t lcv[5] = {};
     if constexpr (LCL && DO_L) {
         const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
-        const uint32_t eo = (uint32_t)e * 4u;
+        // (ablation 8192: from the first workgroup's lines -- their HBM reads gone, timing only)
+        const uint32_t eo = (kAblate & 8192u) ? (uint32_t)lane * 4u : (uint32_t)e * 4u;
 #pragma unroll
         for (int j = 0; j < 5; ++j)
             lcv[j] = __builtin_amdgcn_raw_buffer_load_b32(
@@ -1588,7 +1590,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 v.z &= km.z;
                 v.w &= km.w;
                 // row 4q + lrow; padding rows (>= W) are never dirty
-                const bool dirty = (bdl >> (4 * q)) & 1u && 4 * q + lrow < W;
+                const bool dirty = (bdl >> (4 * q)) & 1u && 4 * q + lrow < W && !(kAblate & 4096u);
                 buf_store16<kNT>(rb, dirty ? boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff, v);
             }
         }
@@ -1671,10 +1673,12 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             // count of the spawned shape (csid, counted above)
             const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
             const uint32_t eo = (uint32_t)e * 4u;
+            // (ablation 2048: the lock-path counter stores dropped, timing only)
+            const bool cst = !(kAblate & 2048u);
             __builtin_amdgcn_raw_buffer_store_b32(
-                mt_out, rs, dr || chunk_me ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff, 0, kNT);
+                mt_out, rs, cst && (dr || chunk_me) ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff, 0, kNT);
             __builtin_amdgcn_raw_buffer_store_b32(
-                (uint32_t)csid, rs, dr ? eo + (uint32_t)(ST_STAT_COUNT0 + sid) * (uint32_t)sd * 4u : kOff, 0, kNT);
+                (uint32_t)csid, rs, cst && dr ? eo + (uint32_t)(ST_STAT_COUNT0 + sid) * (uint32_t)sd * 4u : kOff, 0, kNT);
             if constexpr (VEC) {  // st_step_vec's info snapshot: the shape counts after the step
                 const auto ri = buf_rsrc(p.info, (uint32_t)ST_NSTAT * (uint32_t)p.n * 4u);
 #pragma unroll
@@ -1755,11 +1759,12 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             };
             put(ST_STAT_TIME, time, true);
             put(kPieceRow, (int32_t)pw_out, true);
-            put(ST_STAT_SCORE, score, locknow && score != o_score);
-            put(ST_STAT_LINES, lines, locknow && lines != o_lines);
-            put(ST_STAT_HOLES, holes, locknow && holes != o_holes);
-            put(ST_STAT_PIECE_HEIGHT, height, locknow && height != o_height);
-            put(ST_STAT_DEATHS, deaths, locknow && deaths != o_deaths);
+            const bool cst = !(kAblate & 2048u);  // (ablation: lock-path counter stores dropped)
+            put(ST_STAT_SCORE, score, cst && locknow && score != o_score);
+            put(ST_STAT_LINES, lines, cst && locknow && lines != o_lines);
+            put(ST_STAT_HOLES, holes, cst && locknow && holes != o_holes);
+            put(ST_STAT_PIECE_HEIGHT, height, cst && locknow && height != o_height);
+            put(ST_STAT_DEATHS, deaths, cst && locknow && deaths != o_deaths);
             if constexpr (VEC) {
                 // st_step_vec's info snapshot: this wave's rows for every env
                 // (locking lanes from the registers, the others unchanged)
@@ -1839,11 +1844,12 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             if (p.wire) {
                 // st_step_wire (BASELINE C5's gather format, st_wire_words):
                 // per env one bit stream -- column x's H obs bits at bit x*H,
-                // then the reward's low 16 bits (|reward| < 2^15 for W <= 32,
-                // H <= 28) and done -- as words [j][n], so one gather moves
-                // ceil((W*H + 17) / 32) words per env (10x20: 7, 28 B) instead
-                // of obs + reward + done as W + 2 words (48 B)
-                const auto rw = buf_rsrc(p.wire, (uint32_t)((W * H + 17 + 31) / 32) * (uint32_t)p.n * 4u);
+                // then the reward's 32 bits (lossless: host-written counters
+                // can make a penalise_*_increase reward of any int32) and done
+                // -- as words [j][n], so one gather moves ceil((W*H + 33) / 32)
+                // words per env (10x20: 8, 32 B) instead of obs + reward +
+                // done as W + 2 words (48 B)
+                const auto rw = buf_rsrc(p.wire, (uint32_t)((W * H + 33 + 31) / 32) * (uint32_t)p.n * 4u);
                 uint32_t off = (uint32_t)e * 4u;
                 const uint32_t rowb = (uint32_t)p.n * 4u;
                 uint64_t acc = 0;
@@ -1861,7 +1867,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
 #pragma unroll
                 for (int x = 0; x < (WT ? WT : kMaxW); ++x)
                     if (WT || x < W) put((lcol(L, x, lane) | lcol(sm.OV, x, lane)) & hmask, H);
-                put((uint32_t)rew & 0xFFFFu, 16);
+                put((uint32_t)rew, 32);
                 put(died ? 1u : 0u, 1);
                 if (nb > 0) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)acc, rw, real ? off : kOff, 0, kNT);
             }
@@ -3764,22 +3770,36 @@ hipError_t launch_rollout(const KParams &p, hipStream_t s) {
     return hipGetLastError();
 }
 
-// st_unwire: the wire format (st_step_wire, above) back to packed obs
-// [W][n], reward [n] (sign-extended from 16 bits) and done [n]; one env per
-// thread, words [j][n] coalesced across the wave
-__global__ __launch_bounds__(256) void k_unwire(int W, int H, int64_t n, const uint32_t *__restrict__ wire,
-                                                uint32_t *__restrict__ obs, int32_t *__restrict__ reward,
-                                                uint8_t *__restrict__ done) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n) return;
+// st_unwire / st_unwire_shards: the wire format (st_step_wire, above) of
+// `shards` gathered blocks [shards][words][n_cap] back to packed obs
+// [W][n_global], reward [n_global] and done [n_global] in global env order;
+// shard r holds envs [off_r, off_r + cnt_r) at its columns 0 .. cnt_r - 1,
+// the contiguous blocks of distributed.shard_range (the first n_global %
+// shards shards one env more).  One env per thread, words [j][n_cap]
+// coalesced across the wave, outputs coalesced.
+__global__ __launch_bounds__(256) void k_unwire(int W, int H, int64_t n_global, int shards, int64_t n_cap,
+                                                const uint32_t *__restrict__ wire, uint32_t *__restrict__ obs,
+                                                int32_t *__restrict__ reward, uint8_t *__restrict__ done) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_global) return;
+    const int64_t base = n_global / shards, rem = n_global - base * shards;
+    int64_t r, i;
+    if (g < rem * (base + 1)) {
+        r = g / (base + 1);
+        i = g - r * (base + 1);
+    } else {
+        r = rem + (g - rem * (base + 1)) / base;
+        i = g - rem * (base + 1) - (r - rem) * base;
+    }
+    const int words = (W * H + 33 + 31) / 32;
     const uint32_t hm = (1u << H) - 1u;
-    const uint32_t *src = wire + e;
+    const uint32_t *src = wire + r * (int64_t)words * n_cap + i;
     uint64_t acc = 0;
     int nb = 0;
     auto take = [&](int k) -> uint32_t {  // k <= 32
         if (nb < k) {
             acc |= (uint64_t)*src << nb;
-            src += n;
+            src += n_cap;
             nb += 32;
         }
         const uint32_t v = (uint32_t)acc & (k == 32 ? ~0u : (1u << k) - 1u);
@@ -3787,16 +3807,16 @@ __global__ __launch_bounds__(256) void k_unwire(int W, int H, int64_t n, const u
         nb -= k;
         return v;
     };
-    for (int x = 0; x < W; ++x) obs[(int64_t)x * n + e] = take(H) & hm;
-    reward[e] = (int32_t)(int16_t)(uint16_t)take(16);
-    done[e] = (uint8_t)take(1);
+    for (int x = 0; x < W; ++x) obs[(int64_t)x * n_global + g] = take(H) & hm;
+    reward[g] = (int32_t)take(32);
+    done[g] = (uint8_t)take(1);
 }
 
-hipError_t launch_unwire(int W, int H, int64_t n, const uint32_t *wire, uint32_t *obs, int32_t *reward,
-                         uint8_t *done, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_unwire, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, W, H, n, wire, obs, reward,
-                       done);
+hipError_t launch_unwire(int W, int H, int64_t n_global, int shards, int64_t n_cap, const uint32_t *wire,
+                         uint32_t *obs, int32_t *reward, uint8_t *done, hipStream_t s) {
+    if (n_global <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_unwire, dim3((unsigned)((n_global + 255) / 256)), dim3(256), 0, s, W, H, n_global, shards,
+                       n_cap, wire, obs, reward, done);
     return hipGetLastError();
 }
 

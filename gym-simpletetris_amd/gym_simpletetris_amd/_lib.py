@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ST_LIB") or os.path.join(_HERE, "libsimpletetris.so")
 
 ST_OK, ST_EINVAL, ST_ENOMEM, ST_EHIP, ST_ESTATE = 0, -1, -2, -3, -4
+ABI_VERSION = 2  # ST_ABI_VERSION of include/simpletetris.h
 
 # st_flags (include/simpletetris.h) keyed by the reference kwarg names
 # (TetrisEngine.__init__, tetris_env.py:126-137).
@@ -37,7 +38,7 @@ MT_N = 624
 EXPORT_MT, EXPORT_OBS_F32 = 1, 2  # st_export_env parts
 
 EXPORTS = ("st_create", "st_destroy", "st_seed", "st_reset", "st_step", "st_step_f32", "st_step_vec", "st_rollout",
-           "st_wire_words", "st_step_wire", "st_unwire",
+           "st_wire_words", "st_step_wire", "st_unwire", "st_unwire_shards",
            "st_obs_to_f32", "st_render", "st_grayscale", "st_state", "st_copy", "st_mt_sync", "st_state_bytes", "st_save",
            "st_load", "st_export_env", "st_export_words", "st_check_actions", "st_set_action_flag", "st_stream_sync",
            "st_host_device_ptr", "st_gen_actions", "st_policy_greedy", "st_debug_stamps", "st_last_error", "st_abi_version")
@@ -92,6 +93,7 @@ def load(path: str = LIB_PATH):
         "st_wire_words": ([i32, i32], ctypes.c_int),
         "st_step_wire": ([vp, vp, vp, vp], ctypes.c_int),
         "st_unwire": ([i32, i32, i64, vp, vp, vp, vp, vp], ctypes.c_int),
+        "st_unwire_shards": ([i32, i32, i64, i32, i64, vp, vp, vp, vp, vp], ctypes.c_int),
         "st_obs_to_f32": ([vp, vp, vp, vp], ctypes.c_int),
         "st_render": ([vp, vp, vp], ctypes.c_int),
         "st_grayscale": ([vp, vp, i32, i32, i32, vp, vp], ctypes.c_int),
@@ -120,8 +122,8 @@ def load(path: str = LIB_PATH):
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
-    if L.st_abi_version() != 1:
-        raise ImportError(f"libsimpletetris ABI {L.st_abi_version()} != 1")
+    if L.st_abi_version() != ABI_VERSION and not ab_override:
+        raise ImportError(f"libsimpletetris ABI {L.st_abi_version()} != {ABI_VERSION}")
     _lib = L
     return L
 

@@ -17,10 +17,11 @@ ranks pad their buffer to the longest shard (`shard_cap`) for the transfer and
 
 With `wire=True` (ShardedTetris) each rank steps with st_step_wire straight
 into a [wire_words][n_local] int32 buffer -- per env one bit stream of the
-obs columns, the reward's low 16 bits and done: 7 words (28 B) per 10x20 env
-instead of W + 2 (48 B), so the per-step gather moves 1.7x fewer bytes into
+obs columns, the reward's 32 bits and done: 8 words (32 B) per 10x20 env
+instead of W + 2 (48 B), so the per-step gather moves 1.5x fewer bytes into
 rank 0 -- and rank 0 turns the gathered rows back into (obs, reward, done)
-with st_unwire (`assemble_wire`), bit-exact.
+with st_unwire_shards straight from the receive buffer (`unwire_recv`; or
+`assemble_wire` from a list of per-rank buffers), bit-exact.
 """
 from __future__ import annotations
 
@@ -81,15 +82,16 @@ def gather_outputs(buf: torch.Tensor, group=None, dst: int = 0,
 
 def assemble(bufs: List[torch.Tensor], width: int, counts: Optional[List[int]] = None):
     """Rank-0 side: concatenate gathered buffers into global (obs [W][N],
-    reward [N], done [N]) in global env order; `counts[r]` = rank r's real
-    envs (shard_range), default every column of every buffer."""
+    reward [N], done bool [N]) in global env order; `counts[r]` = rank r's
+    real envs (shard_range), default every column of every buffer.  done is
+    torch.bool, as from the wire format's assemble_wire / unwire_recv."""
     counts = [b.shape[1] for b in bufs] if counts is None else counts
     if len(counts) != len(bufs):
         raise ValueError(f"{len(counts)} counts for {len(bufs)} buffers")
     obs = torch.cat([b[:width, :c] for b, c in zip(bufs, counts)], dim=1)
     reward = torch.cat([b[width, :c] for b, c in zip(bufs, counts)])
     done = torch.cat([buffer_views(b, width)[2][:c] for b, c in zip(bufs, counts)])
-    return obs, reward, done
+    return obs, reward, done.view(torch.bool)
 
 
 def assemble_wire(bufs: List[torch.Tensor], width: int, height: int,
@@ -107,6 +109,15 @@ def assemble_wire(bufs: List[torch.Tensor], width: int, height: int,
         dev = torch.device("cuda", torch.cuda.current_device())
     wire = torch.cat([b[:, :c].to(dev) for b, c in zip(bufs, counts)], dim=1).contiguous()
     return unwire(wire, width, height)
+
+
+def unwire_recv(recv: torch.Tensor, width: int, height: int, n_global: int, out=None):
+    """Rank-0 side of the wire format, straight from one contiguous receive
+    buffer int32 [world, words, n_cap] on the GPU (gather into its views
+    recv[r]) -> global (obs [W][N], reward [N], done bool [N]) in global env
+    order, by st_unwire_shards (no concatenation)."""
+    from .engine import unwire_shards
+    return unwire_shards(recv, width, height, n_global, out=out)
 
 
 class ShardedTetris:

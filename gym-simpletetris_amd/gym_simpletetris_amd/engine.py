@@ -320,7 +320,7 @@ class TetrisBatch:
     def step_wire(self, actions, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """One step (as step()) writing BASELINE C5's gather format instead
         of obs / reward / done: int32 [wire_words, n], per env column x's obs
-        bits at bit x*H, then the reward's low 16 bits and done
+        bits at bit x*H, then the reward's 32 bits and done
         (st_step_wire; `unwire` restores step()'s outputs bit-exactly)."""
         a = self._actions(actions)
         shape = (self.wire_words, self.n)
@@ -532,4 +532,29 @@ def unwire(wire: torch.Tensor, width: int, height: int):
     with torch.cuda.device(wire.device):
         C.check(L.st_unwire(width, height, n, _ptr(wire), _ptr(obs), _ptr(reward), _ptr(done),
                             _stream_ptr(wire.device)))
+    return obs, reward, done
+
+
+def unwire_shards(recv: torch.Tensor, width: int, height: int, n_global: int, out=None):
+    """st_unwire_shards: a gather's receive buffer int32 [shards, words,
+    n_cap] on a GPU (shard r = the contiguous block shard_range(n_global,
+    shards, r), its envs at columns 0 .. count_r - 1) -> (packed obs int32
+    [width, n_global], reward int32 [n_global], done bool [n_global]) in
+    global env order, bit-exact with step()'s outputs, without assembling the
+    shards first.  `out`: optional (obs, reward, done) tensors to write.
+    Runs on the tensor's device, on torch's current stream."""
+    L = C.load()
+    words = C.check_count(L.st_wire_words(width, height))
+    if not isinstance(recv, torch.Tensor) or recv.device.type != "cuda" or recv.dtype != torch.int32 \
+            or recv.dim() != 3 or recv.shape[1] != words or not recv.is_contiguous():
+        raise ValueError(f"recv must be a contiguous int32 [shards, {words}, n_cap] GPU tensor")
+    shards, _, cap = recv.shape
+    if out is None:
+        out = (torch.empty((width, n_global), dtype=torch.int32, device=recv.device),
+               torch.empty(n_global, dtype=torch.int32, device=recv.device),
+               torch.empty(n_global, dtype=torch.bool, device=recv.device))
+    obs, reward, done = out
+    with torch.cuda.device(recv.device):
+        C.check(L.st_unwire_shards(width, height, n_global, shards, cap, _ptr(recv), _ptr(obs), _ptr(reward),
+                                   _ptr(done), _stream_ptr(recv.device)))
     return obs, reward, done

@@ -292,15 +292,28 @@ class TetrisEnv:
 
 
 class _Slot:
-    """One set of st_step_vec outputs (the vector env alternates two)."""
+    """One set of st_step_vec outputs: with copy=False the vector env
+    alternates two; with copy=True every step gets a fresh one, handed to
+    the caller (the env never writes it again).  The int32 outputs are views
+    of ONE allocation (obs | reward | done bytes | final obs | info rows), the
+    float32 obs a second one: two caching-allocator calls per step."""
 
     def __init__(self, n, width, height, dev, f32, final):
-        self.obs = torch.zeros((width, n), dtype=torch.int32, device=dev)
-        self.obs_f32 = torch.zeros((n, width, height), dtype=torch.float32, device=dev) if f32 else None
-        self.reward = torch.zeros(n, dtype=torch.int32, device=dev)
-        self.done = torch.zeros(n, dtype=torch.bool, device=dev)
-        self.final = torch.zeros((width, n), dtype=torch.int32, device=dev) if final else None
-        self.info = torch.zeros((C.NSTAT, n), dtype=torch.int32, device=dev)
+        nd = (n + 3) // 4  # int32 words holding done's n bytes
+        rows = width + (width if final else 0) + C.NSTAT + 1
+        flat = torch.empty(rows * n + nd, dtype=torch.int32, device=dev)
+        # whole rows first: obs and the final obs start 16-B aligned whenever
+        # n % 4 == 0 (the step kernel's 16-B store path)
+        self.obs = flat[:width * n].view(width, n)
+        o = width * n
+        self.final = flat[o:o + width * n].view(width, n) if final else None
+        o += width * n if final else 0
+        self.info = flat[o:o + C.NSTAT * n].view(C.NSTAT, n)
+        o += C.NSTAT * n
+        self.reward = flat[o:o + n]
+        o += n
+        self.done = flat[o:o + nd].view(torch.uint8)[:n].view(torch.bool)
+        self.obs_f32 = torch.empty((n, width, height), dtype=torch.float32, device=dev) if f32 else None
         self.ptrs = tuple(None if t is None else ctypes.c_void_p(t.data_ptr()) for t in
                           (self.obs, self.obs_f32, self.reward, self.done, self.final, self.info))
         self.owner = None  # weakref to the VecInfo that reads this slot
@@ -318,10 +331,11 @@ class VecInfo:
     which envs those are).
 
     The step kernel writes the counters into the slot this info reads, so
-    building it costs nothing per step; the env reuses a slot two steps later
-    and copies it into this object first if this info is still alive then
-    (a counter tensor taken out of the info and kept past that is a view of
-    the slot: clone it to keep it)."""
+    building it costs nothing per step.  With copy=True (the default) the
+    slot is the caller's; with copy=False the env reuses a slot two steps
+    later and copies it into this object first if this info is still alive
+    then (a counter tensor taken out of the info and kept past that is a
+    view of the slot: clone it to keep it)."""
 
     def __init__(self, env: "TetrisVecEnv", slot: _Slot):
         self._env = env
@@ -387,9 +401,18 @@ class TetrisVecEnv:
     the terminal observation itself (no final_observation key).
     info['ep_score'] / ['ep_lines'] / ['ep_time'] / ['ep_holes'] hold the
     finished episode's counters.  One st_step_vec launch per step writes the
-    obs, reward, done, the terminal obs and the info counters; the returned
-    tensors live in one of two output slots that alternate, so they stay
-    valid until two steps later (an info object kept longer takes a copy).
+    obs, reward, done, the terminal obs and the info counters.  copy=True
+    (default; gym's SyncVectorEnv convention, and the reference's step
+    returns a fresh np.copy of the board, tetris_env.py:302): the kernel
+    writes them into tensors allocated for this step, which the env never
+    touches again -- obs / reward / done / info stay valid as long as the
+    caller keeps them.  copy=False: they live in one of two output slots
+    that alternate, so they are overwritten two steps later (an info object
+    kept longer takes a copy; the obs / reward / done tensors do not) -- the
+    fast path, for loops that consume each step's outputs right away.
+    reset(return_info=True) returns (obs, info) like the reference's
+    reset (:405-411): the post-reset counters (time 0, score 0, the new
+    current_piece, the persisting deaths and statistics).
     Actions outside 0..6 raise KeyError like the reference's.  By default
     (`validate_actions='async'`) the step kernel checks the actions it loads
     anyway and sets a sticky flag in mapped host memory: no extra launch and
@@ -407,7 +430,8 @@ class TetrisVecEnv:
                  advanced_clears=False, high_scoring=False, penalise_holes=False,
                  penalise_holes_increase=False, lock_delay=0, step_reset=False, *,
                  device=None, seed: int = 0, global_offset: int = 0, autoreset: bool = True,
-                 autoreset_obs: str = "reset", obs_format: str = "f32", validate_actions="async"):
+                 autoreset_obs: str = "reset", obs_format: str = "f32", validate_actions="async",
+                 copy: bool = True):
         if obs_format not in ("f32", "packed"):
             raise ValueError("obs_format must be 'f32' or 'packed'")
         if autoreset_obs not in ("reset", "terminal"):
@@ -431,7 +455,10 @@ class TetrisVecEnv:
         self.device = self.engine.device
         self._want_f32 = obs_format == "f32" and obs_type == "ram"
         fin = self.autoreset and autoreset_obs == "reset"
-        self._slots = [_Slot(self.num_envs, width, height, self.device, self._want_f32, fin) for _ in range(2)]
+        self.copy = bool(copy)
+        self._fin = fin
+        self._slots = [] if self.copy else \
+            [_Slot(self.num_envs, width, height, self.device, self._want_f32, fin) for _ in range(2)]
         self._k = 0
         self._step_vec = self.engine._L.st_step_vec
 
@@ -445,27 +472,44 @@ class TetrisVecEnv:
         g = self.engine.grayscale(packed, 84, ch)
         return g if (self.obs_type == "rgb" or self.extend_dims) else g.squeeze(-1)
 
-    def reset(self):
+    def reset(self, return_info: bool = False):
+        """TetrisEnv.reset (tetris_env.py:405-411) for every env: clear()
+        (:306-315), whose observation is the empty board; with return_info
+        also get_info() after the reset (:232-241) as a dict of [N] tensors
+        (ep_* 0: no episode finished in a reset)."""
         self.engine.reset()
         zeros = torch.zeros((self.width, self.num_envs), dtype=torch.int32, device=self.device)
         if self.obs_format == "packed":
-            return zeros
-        return self._obs(zeros, torch.zeros((self.num_envs, self.width, self.height),
-                                            device=self.device) if self.obs_type == "ram" else None)
+            obs = zeros
+        else:
+            obs = self._obs(zeros, torch.zeros((self.num_envs, self.width, self.height),
+                                               device=self.device) if self.obs_type == "ram" else None)
+        if not return_info:
+            return obs
+        st = self.engine.state_tensors(("stats",), sync=False)["stats"][:, :self.num_envs].clone()
+        for k in ("ep_time", "ep_score", "ep_lines", "ep_holes"):
+            st[C.STAT[k]] = 0
+        info = self.engine.info_tensors(st)
+        info["current_piece"] = st[C.STAT["piece"]] & 7
+        return obs, info
 
     def step(self, actions):
         eng = self.engine
         a = eng._actions(actions)
-        slot = self._slots[self._k]
-        self._k ^= 1
-        held = slot.owner() if slot.owner is not None else None
-        if held is not None:  # an info from two steps ago is still alive: it keeps a copy
-            held._detach()
+        if self.copy:  # this step's outputs, the caller's from now on
+            slot = _Slot(self.num_envs, self.width, self.height, self.device, self._want_f32, self._fin)
+        else:
+            slot = self._slots[self._k]
+            self._k ^= 1
+            held = slot.owner() if slot.owner is not None else None
+            if held is not None:  # an info from two steps ago is still alive: it keeps a copy
+                held._detach()
         po, pf, pr, pd, pfin, pinfo = slot.ptrs
         C.check(self._step_vec(eng._ctx, ctypes.c_void_p(a.data_ptr()), po, pf, pr, pd, pfin, pinfo,
                                eng._stream()))
         info = VecInfo(self, slot)
-        slot.owner = weakref.ref(info)
+        if not self.copy:
+            slot.owner = weakref.ref(info)
         return self._obs(slot.obs, slot.obs_f32), slot.reward, slot.done, info
 
     def check_actions(self):

@@ -31,7 +31,10 @@
 extern "C" {
 #endif
 
-#define ST_ABI_VERSION 1
+/* 2: st_step_wire carries the reward's 32 bits (st_wire_words grew by one
+ * word for 10x20), st_unwire_shards.  Snapshots (st_save) keep their own
+ * format version, unchanged. */
+#define ST_ABI_VERSION 2
 
 typedef struct st_ctx st_ctx;
 typedef void *st_stream; /* hipStream_t */
@@ -159,7 +162,8 @@ int st_step_f32(st_ctx *ctx, const uint8_t *d_actions, uint32_t *d_obs, float *d
  *     observation (what the reference's step returned, :301-302) is written
  *     to d_final_obs.  Only the columns of such envs are meaningful (the
  *     kernel writes 16-B groups holding one).  NULL: the terminal obs is
- *     returned in d_obs (st_step's convention).
+ *     returned in d_obs (st_step's convention).  d_final_obs requires d_obs
+ *     (ST_EINVAL otherwise).
  *   d_info (int32 [ST_NSTAT][n_envs], or NULL): every counter row after the
  *     step (get_info, :232-241, from one snapshot written by the step
  *     kernel): rows ST_STAT_* as in st_state_views.stats except
@@ -175,20 +179,28 @@ int st_step_vec(st_ctx *ctx, const uint8_t *d_actions, uint32_t *d_obs, float *d
 /* BASELINE C5's gather format.  st_step_wire is st_step writing, instead of
  * obs / reward / done, one bit stream per env: column x's `height` obs bits
  * (exactly st_step's packed obs word x) at bit x*height, then the reward's
- * low 16 bits (two's complement; |reward| < 2^15 for every flag set with
- * width <= 32, height <= 28) and the done bit -- stored as
- * st_wire_words(width, height) = ceil((width*height + 17) / 32) uint32 rows
- * d_wire [words][n_envs] (10x20: 7 words, 28 B per env, against 48 B for
+ * 32 bits (two's complement: lossless for every int32 the step computes,
+ * host-written counters included) and the done bit -- stored as
+ * st_wire_words(width, height) = ceil((width*height + 33) / 32) uint32 rows
+ * d_wire [words][n_envs] (10x20: 8 words, 32 B per env, against 48 B for
  * obs + reward + done as width + 2 rows), so a per-step gather of every
  * shard's outputs to rank 0 (tetris_env.py:397-403's return values, for all
- * envs) moves 1.7x fewer bytes over xGMI.  st_unwire turns gathered wire
- * rows back into st_step's outputs (d_obs uint32 [width][n], d_reward int32
- * [n], d_done uint8 [n]), bit-exact.  st_wire_words returns ST_EINVAL for a
- * board outside 1..32 x 1..28. */
+ * envs) moves 1.5x fewer bytes over xGMI.  st_unwire turns wire rows back
+ * into st_step's outputs (d_obs uint32 [width][n], d_reward int32 [n],
+ * d_done uint8 [n]), bit-exact.  st_unwire_shards does the same straight from
+ * a gather's receive buffer: d_wire [shards][words][n_cap], shard r's envs at
+ * its columns 0 .. count_r - 1, where shard r holds the contiguous global
+ * block of distributed.shard_range (counts n_global / shards, the first
+ * n_global % shards shards one more; n_cap >= the largest count) -> d_obs
+ * [width][n_global], d_reward [n_global], d_done [n_global] in global env
+ * order.  st_wire_words returns ST_EINVAL for a board outside 1..32 x 1..28. */
 int st_wire_words(int32_t width, int32_t height);
 int st_step_wire(st_ctx *ctx, const uint8_t *d_actions, uint32_t *d_wire, st_stream stream);
 int st_unwire(int32_t width, int32_t height, int64_t n, const uint32_t *d_wire, uint32_t *d_obs,
               int32_t *d_reward, uint8_t *d_done, st_stream stream);
+int st_unwire_shards(int32_t width, int32_t height, int64_t n_global, int32_t shards, int64_t n_cap,
+                     const uint32_t *d_wire, uint32_t *d_obs, int32_t *d_reward, uint8_t *d_done,
+                     st_stream stream);
 
 /* k consecutive st_step calls in ONE launch: the driver loop of README.md:43-51
  * (`for t: obs, r, done, info = env.step(a[t])`) with all actions known up
@@ -263,7 +275,7 @@ int st_mt_sync(st_ctx *ctx, st_stream stream);
  * and its MT19937 state (CPython random.getstate(), :187).
  * st_state_bytes: the size of one snapshot of this context.
  * st_save: writes it to host memory (a 64-byte header -- magic "STSNAP\0\1",
- *   ABI version, width, height, ST_NSTAT, n_envs -- then board uint32
+ *   snapshot format version (1), width, height, ST_NSTAT, n_envs -- then board uint32
  *   [width][n_envs], stats int32 [ST_NSTAT][n_envs], mt uint32 [n_envs][624]).
  * st_load: restores one into a context with the same width, height and
  *   n_envs (scoring flags and lock delay are configuration, not state, and

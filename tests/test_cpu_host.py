@@ -36,11 +36,11 @@ def test_host_only_abi_functions_and_constants():
     the Python binding mirrors."""
     from gym_simpletetris_amd import _lib
     L = _lib.load()
-    assert L.st_abi_version() == 1
+    assert L.st_abi_version() == _lib.ABI_VERSION == 2
     assert L.st_export_words(10, 20) == 10 + 2 + _lib.NSTAT + _lib.MT_N + 200
     assert L.st_export_words(4, 4) == 4 + 2 + _lib.NSTAT + _lib.MT_N + 16
     # the C5 gather format: ceil((W*H + 17) / 32) words per env
-    assert L.st_wire_words(10, 20) == 7 and L.st_wire_words(32, 28) == 29 and L.st_wire_words(4, 4) == 2
+    assert L.st_wire_words(10, 20) == 8 and L.st_wire_words(32, 28) == 30 and L.st_wire_words(4, 4) == 2
     assert L.st_wire_words(0, 20) == _lib.ST_EINVAL and L.st_wire_words(10, 29) == _lib.ST_EINVAL
     assert L.st_unwire(10, 20, -1, None, None, None, None, None) == _lib.ST_EINVAL
     src = open(os.path.join(ROOT, "include", "simpletetris.h")).read()
@@ -164,7 +164,7 @@ def _gather_worker(rank, world, port, q, n_global):
     if rank == 0:
         o, r, d = assemble(bufs, W, [shard_range(n_global, world, i)[1] for i in range(world)])
         ok = (torch.equal(r, -torch.arange(n_global, dtype=torch.int32))
-              and torch.equal(d, (torch.arange(n_global) % 3 == 0).to(torch.uint8))
+              and d.dtype == torch.bool and torch.equal(d, torch.arange(n_global) % 3 == 0)
               and torch.equal(o[3], torch.arange(n_global, dtype=torch.int32) * 16 + 3))
         q.put(ok)
     dist.destroy_process_group()

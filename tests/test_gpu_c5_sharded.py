@@ -164,9 +164,10 @@ def test_c5_eight_ranks_ragged(tmp_path):
 def test_bench_gpus8_direct_invocation(tmp_path):
     """`python bench.py --gpus 8` run directly: it spawns its 8 ranks itself
     (the driver's C5 launch path, here all on cuda:0 over gloo); every timed
-    step is st_step on each shard + the gather to rank 0 (K gathers inside
-    the region), and rank 0's assembled outputs of the last timed step equal
-    the oracle stepping all 8 x 2,048 envs.  Rank 0 prints one JSON line."""
+    step is st_step_wire on each shard + the gather to rank 0 + rank 0's
+    decode of the gathered rows (K gathers and K decodes inside the region),
+    and rank 0's decoded outputs of the last timed step equal the oracle
+    stepping all 8 x 2,048 envs.  Rank 0 prints one JSON line."""
     from test_gpu_multirank import check_bench_dump
     dump = tmp_path / "c5.npz"
     env = dict(os.environ, ST_BENCH_SHARED_GPU="1", ST_BENCH_DUMP=str(dump))
@@ -181,10 +182,13 @@ def test_bench_gpus8_direct_invocation(tmp_path):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 8 and d["config"]["envs_total"] == 8 * 2048
     assert d["value"] > 0 and d["gather"]["gathers_in_timed_region"] == 20
-    # the default gather format: st_step_wire's 7 rows per env, not W + 2
-    assert d["gather"]["bytes_per_rank_per_step"] == 7 * 2048 * 4
+    # the default gather format: st_step_wire's 8 rows per env, not W + 2
+    assert d["gather"]["bytes_per_rank_per_step"] == 8 * 2048 * 4
+    # rank 0 decoded every timed step's gathered rows inside the region
+    assert d["gather"]["decodes_in_timed_region_rank0"] == 20
+    assert d["gather"]["no_decode"]["value"] > 0
     assert d["gather"]["format"].startswith("st_step_wire")
     assert d["config"]["workload"].startswith("C5:")
     assert d["scaling"] == "weak"
-    z = check_bench_dump(dump, 8 * 2048, 25)
-    assert int(z["gathers_timed"]) == 20
+    z = check_bench_dump(dump, 8 * 2048, 25)  # the region's own last decode vs the oracle
+    assert int(z["gathers_timed"]) == 20 and int(z["decodes_timed"]) == 20

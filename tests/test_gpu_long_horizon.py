@@ -47,7 +47,8 @@ class ParallelOracle:
         parts = parts or _threads()
         bounds = np.linspace(0, n, parts + 1).astype(int)
         self.sl = [(int(a), int(b)) for a, b in zip(bounds[:-1], bounds[1:]) if b > a]
-        self.obs = [O.OracleBatch(b - a, [SEED_BASE + a + e for e in range(b - a)], width=W, height=H, **kw)
+        kw = dict(dict(width=W, height=H), **kw)  # (a board other than 10x20: width / height in kw)
+        self.obs = [O.OracleBatch(b - a, [SEED_BASE + a + e for e in range(b - a)], **kw)
                     for a, b in self.sl]
         for ob in self.obs:
             ob.reset()

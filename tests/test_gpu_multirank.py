@@ -143,5 +143,7 @@ def test_bench_rccl_calls_one_rank(tmp_path):
     assert p.returncode == 0, p.stderr[-2000:]
     d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert d["gather"]["backend"] == "nccl" and d["gather"]["gathers_in_timed_region"] == 30
+    assert d["gather"]["decodes_in_timed_region_rank0"] == 30  # wire format: decoded inside the region
     assert d["value"] > 0
-    check_bench_dump(tmp_path / "c5.npz", 8192, 35)
+    z = check_bench_dump(tmp_path / "c5.npz", 8192, 35)
+    assert int(z["decodes_timed"]) == 30

@@ -67,7 +67,7 @@ def test_library_is_the_hip_build():
     G = _engine()
     from gym_simpletetris_amd import _lib
     L = _lib.load()
-    assert L.st_abi_version() == 1
+    assert L.st_abi_version() == C.ABI_VERSION
     b = G.TetrisBatch(3, seeds=[1, 2, 3])
     b.reset()
     b.step(np.zeros(3, np.uint8))

@@ -26,9 +26,12 @@ pytestmark = pytest.mark.gpu
 W, H = 10, 20
 
 
-def _unpack_f32(words):
-    """packed obs [n][W] u32 -> float32 [n][W][H]."""
-    return ((words[:, :, None] >> np.arange(H, dtype=np.uint32)) & 1).astype(np.float32)
+C4 = dict(advanced_clears=True, penalise_holes_increase=True, penalise_height_increase=True)
+
+
+def _unpack_f32(words, h=H):
+    """packed obs [n][W] u32 -> float32 [n][W][h]."""
+    return ((words[:, :, None] >> np.arange(h, dtype=np.uint32)) & 1).astype(np.float32)
 
 
 def _check_info(info, ref_st, done, t):
@@ -46,19 +49,20 @@ def _check_info(info, ref_st, done, t):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("n", [65536, 1001])
-def test_vec_env_conventions_vs_oracle(n):
+@pytest.mark.parametrize("n,w,h,kw", [(65536, 10, 20, {}), (1001, 10, 20, {}), (1001, 9, 15, C4)])
+def test_vec_env_conventions_vs_oracle(n, w, h, kw):
     """Both conventions side by side, packed obs, every step checked: reward,
     done, returned obs, final_observation and the info counters; at the end
     the shape counts and current piece of every env.  n = 1,001 runs the
-    ragged store path (n % 4 != 0)."""
+    ragged store path (n % 4 != 0); 9x15 with the C4 scoring flags the
+    runtime-size vector kernel (k_step<0, 0, ..., VEC>)."""
     G = _engine()
     T = 300 if n == 65536 else 400
-    a = G.TetrisVecEnv(n, seed=SEED_BASE, obs_format="packed")  # autoreset_obs='reset'
-    b = G.TetrisVecEnv(n, seed=SEED_BASE, obs_format="packed", autoreset_obs="terminal")
+    a = G.TetrisVecEnv(n, width=w, height=h, seed=SEED_BASE, obs_format="packed", **kw)  # autoreset_obs='reset'
+    b = G.TetrisVecEnv(n, width=w, height=h, seed=SEED_BASE, obs_format="packed", autoreset_obs="terminal", **kw)
     a.reset()
     b.reset()
-    orc = ParallelOracle(n, {})
+    orc = ParallelOracle(n, dict(kw, width=w, height=h))
     acts = torch.empty(n, dtype=torch.uint8, device=a.device)
     CH = 50
     ndone = 0
@@ -99,20 +103,23 @@ def test_vec_env_conventions_vs_oracle(n):
 
 
 @pytest.mark.timeout(200)
-@pytest.mark.parametrize("obs_type", ["ram", "grayscale"])
-def test_vec_env_f32_and_image_conventions(obs_type):
+@pytest.mark.parametrize("obs_type,n,w,h,kw", [("ram", 4096, 10, 20, {}), ("grayscale", 4096, 10, 20, {}),
+                                               ("ram", 1001, 9, 15, C4)])
+def test_vec_env_f32_and_image_conventions(obs_type, n, w, h, kw):
     """float32 ram obs (fused in the step kernel) and grayscale obs under the
     reset convention: the returned obs of a done env is the reset obs (zeros /
     the empty board's image) and final_observation is the terminal obs in the
-    same format; the rest equals the packed path's conversion."""
+    same format; the rest equals the packed path's conversion.  9x15, n =
+    1,001, C4 flags: the runtime-size kernel's generic float32 writer with
+    the reset mask (its KM-masked word path)."""
     G = _engine()
-    n, T = 4096, 200
-    a = G.TetrisVecEnv(n, seed=SEED_BASE, obs_type=obs_type)
-    p = G.TetrisVecEnv(n, seed=SEED_BASE, obs_format="packed", autoreset_obs="terminal")
+    T = 200
+    a = G.TetrisVecEnv(n, width=w, height=h, seed=SEED_BASE, obs_type=obs_type, **kw)
+    p = G.TetrisVecEnv(n, width=w, height=h, seed=SEED_BASE, obs_format="packed", autoreset_obs="terminal", **kw)
     a.reset()
     p.reset()
     acts = torch.empty(n, dtype=torch.uint8, device=a.device)
-    empty = torch.zeros((W, n), dtype=torch.int32, device=a.device)
+    empty = torch.zeros((w, n), dtype=torch.int32, device=a.device)
     saw = 0
     for t in range(T):
         a.engine.gen_actions(t, ASEED, out=acts)
@@ -123,8 +130,8 @@ def test_vec_env_f32_and_image_conventions(obs_type):
         ret = torch.where(dp.unsqueeze(0), empty, op)
         fin = torch.where(dp.unsqueeze(0), op, empty)
         if obs_type == "ram":
-            want = torch.from_numpy(_unpack_f32(ret.cpu().numpy().view(np.uint32).T)).to(a.device)
-            wfin = torch.from_numpy(_unpack_f32(fin.cpu().numpy().view(np.uint32).T)).to(a.device)
+            want = torch.from_numpy(_unpack_f32(ret.cpu().numpy().view(np.uint32).T, h)).to(a.device)
+            wfin = torch.from_numpy(_unpack_f32(fin.cpu().numpy().view(np.uint32).T, h)).to(a.device)
         else:
             want = p.engine.grayscale(ret, 84, 1).squeeze(-1)
             wfin = p.engine.grayscale(fin, 84, 1).squeeze(-1)
@@ -139,12 +146,13 @@ def test_vec_env_f32_and_image_conventions(obs_type):
 
 
 def test_vec_env_info_kept_across_steps():
-    """An info held past later steps still reports its own step (VERDICT r3
-    "next" #4): the env reuses an output slot two steps later and gives the
-    info object a copy first; one not held costs nothing."""
+    """copy=False (the fast path): an info held past later steps still
+    reports its own step (VERDICT r3 "next" #4): the env reuses an output
+    slot two steps later and gives the info object a copy first; one not
+    held costs nothing."""
     G = _engine()
     n = 2048
-    v = G.TetrisVecEnv(n, seed=7, obs_format="packed")
+    v = G.TetrisVecEnv(n, seed=7, obs_format="packed", copy=False)
     v.reset()
     for t in range(30):
         v.step(v.engine.gen_actions(t, 5))
@@ -163,4 +171,64 @@ def test_vec_env_info_kept_across_steps():
     # every info of the loop still reports its own step (each was detached in turn)
     for i, (inf, tm) in enumerate(zip(infos, lives)):
         assert torch.equal(inf["time"], tm), i
+    v.close()
+
+
+@pytest.mark.parametrize("obs_format", ["packed", "f32"])
+def test_vec_env_outputs_kept_across_steps(obs_format):
+    """copy=True (the default, gym's SyncVectorEnv convention; the reference
+    returns a fresh np.copy each step, tetris_env.py:302): step t's obs /
+    reward / done / info held across three later steps are unchanged, and
+    equal a copy=False twin's outputs cloned at step t."""
+    G = _engine()
+    n = 4096
+    v = G.TetrisVecEnv(n, seed=11, obs_format=obs_format)
+    u = G.TetrisVecEnv(n, seed=11, obs_format=obs_format, copy=False)
+    assert v.copy and not u.copy
+    v.reset()
+    u.reset()
+    held = []
+    for t in range(40):
+        acts = v.engine.gen_actions(t, 5).clone()
+        ov, rv, dv, iv = v.step(acts)
+        ou, ru, du, iu = u.step(acts)
+        snap = (ou.clone(), ru.clone(), du.clone(), iu["time"].clone(), iu["final_observation"].clone())
+        held.append(((ov, rv, dv, iv), snap))
+        if len(held) > 4:
+            (o, r, d, i), (so, sr, sd, stime, sfin) = held.pop(0)  # step t - 4's, after four later steps
+            assert torch.equal(o, so) and torch.equal(r, sr) and torch.equal(d, sd), t
+            assert torch.equal(i["time"], stime) and torch.equal(i["final_observation"], sfin), t
+    v.close()
+    u.close()
+
+
+def test_vec_env_reset_return_info_vs_oracle():
+    """reset(return_info=True) (tetris_env.py:405-411): (obs, info) with the
+    post-clear() counters -- time / score / lines / holes / piece_height 0,
+    the new current_piece, deaths and statistics kept (:306-315) -- equal
+    the oracle's after the same steps and a reset of every env."""
+    G = _engine()
+    n, T = 2048, 150
+    v = G.TetrisVecEnv(n, seed=SEED_BASE, obs_format="packed", **C4)
+    obs0, info0 = v.reset(return_info=True)
+    assert int(info0["time"].abs().sum()) == 0 and int(obs0.abs().sum()) == 0
+    orc = ParallelOracle(n, C4)
+    try:
+        orc.rollout(0, T, obs=False)
+        acts = torch.empty(n, dtype=torch.uint8, device=v.device)
+        for t in range(T):
+            v.engine.gen_actions(t, ASEED, out=acts)
+            v.step(acts)
+        obs, info = v.reset(return_info=True)
+        for ob in orc.obs:
+            ob.reset()
+        ref = orc.final_state()
+    finally:
+        orc.close()
+    assert int(obs.abs().sum()) == 0
+    for k, f in (("time", "time"), ("score", "score"), ("lines_cleared", "lines_cleared"), ("holes", "holes"),
+                 ("piece_height", "piece_height"), ("deaths", "n_deaths"), ("current_piece", "shape_id")):
+        assert np.array_equal(info[k].cpu().numpy(), ref[f]), k
+    assert np.array_equal(info["statistics"].cpu().numpy().T, ref["counts"])
+    assert int(info["deaths"].sum()) > 0 and int(info["ep_score"].abs().sum()) == 0
     v.close()

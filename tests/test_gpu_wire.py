@@ -1,13 +1,16 @@
 """BASELINE C5's gather format (st_step_wire / st_unwire, include/simpletetris.h).
 
 st_step_wire is st_step writing one bit stream per env -- the obs columns,
-the reward's low 16 bits, done -- instead of obs / reward / done rows.  Checked
+the reward's 32 bits, done -- instead of obs / reward / done rows.  Checked
 here: (1) step_wire and step on twin batches agree bit-exactly every step
 (unwire(step_wire) == step, and the raw rows == a numpy packing of step's
 outputs), with deaths, same-step resets, clears and every reward flag that
 makes rewards large or negative; the compile-time 10x20 kernel and the
 generic (runtime W, H) one, ragged n; (2) the final states agree; (3) the
-oracle agrees with unwire(step_wire) at full size (65,536 envs, C3).
+oracle agrees with unwire(step_wire) at full size (65,536 envs, C3); (4)
+rewards far beyond 16 bits (host-written holes / piece_height under the
+penalise_*_increase flags) cross the wire intact; (5) st_unwire_shards
+decodes a gather's receive buffer (ragged shards) into global order.
 """
 import numpy as np
 import pytest
@@ -21,16 +24,16 @@ pytestmark = pytest.mark.gpu
 def pack_np(obs, rew, done, W, H):
     """numpy restatement of the wire layout: [words][n] uint32."""
     n = obs.shape[1]
-    words = (W * H + 17 + 31) // 32
+    words = (W * H + 33 + 31) // 32
     bits = np.zeros((n, words * 32), np.uint8)
     for x in range(W):
         col = obs[x].astype(np.uint64)
         for y in range(H):
             bits[:, x * H + y] = (col >> np.uint64(y)) & np.uint64(1)
-    r16 = rew.astype(np.int64) & 0xFFFF
-    for b in range(16):
-        bits[:, W * H + b] = (r16 >> b) & 1
-    bits[:, W * H + 16] = done.astype(np.uint8)
+    r32 = rew.astype(np.int64) & 0xFFFFFFFF
+    for b in range(32):
+        bits[:, W * H + b] = (r32 >> b) & 1
+    bits[:, W * H + 32] = done.astype(np.uint8)
     w = np.zeros((words, n), np.uint64)
     for j in range(words):
         for b in range(32):
@@ -53,7 +56,7 @@ def test_step_wire_equals_step(W, H, n, kw):
     b = G.TetrisBatch(n, width=W, height=H, autoreset="same_step", seeds=seeds, **kw)
     a.reset()
     b.reset()
-    assert b.wire_words == (W * H + 17 + 31) // 32
+    assert b.wire_words == (W * H + 33 + 31) // 32
     deaths = 0
     neg = 0
     for t in range(400):
@@ -95,6 +98,68 @@ def test_step_wire_full_size_vs_oracle():
         assert np.array_equal(r.cpu().numpy(), ref["reward"][t]), t
         assert np.array_equal(d.cpu().numpy().astype(np.uint8), ref["done"][t]), t
         assert np.array_equal(o.cpu().numpy().view(np.uint32).T, ref["obs"][t]), t
+
+
+def test_step_wire_large_rewards_vs_oracle():
+    """Host-written holes / piece_height (st_set_state; the reference accepts
+    any int there) make penalise_holes_increase / penalise_height_increase
+    rewards of +-10^5..10^7 at the next lock (tetris_env.py:288-297):
+    unwire(step_wire) == step == the oracle, every step."""
+    import gym_simpletetris_amd as G
+    from gym_simpletetris_amd import _lib as C
+    from gym_simpletetris_amd.engine import unwire
+    n, steps = 256, 120
+    kw = dict(penalise_holes_increase=True, penalise_height_increase=True)
+    seeds = [300 + e for e in range(n)]
+    a = G.TetrisBatch(n, autoreset="same_step", seeds=seeds, **kw)
+    b = G.TetrisBatch(n, autoreset="same_step", seeds=seeds, **kw)
+    ob = O.OracleBatch(n, seeds, **kw)
+    a.reset()
+    b.reset()
+    ob.reset()
+    st = a.get_state(("stats",))["stats"]
+    holes = np.where(np.arange(n) % 2 == 0, 100000 + 37 * np.arange(n), 0).astype(np.int32)
+    height = np.where(np.arange(n) % 2 == 1, -200000 - 91 * np.arange(n), 0).astype(np.int32)
+    st[C.STAT["holes"]] = holes
+    st[C.STAT["piece_height"]] = height
+    a.set_state(stats=st)
+    b.set_state(stats=st.copy())
+    for i in range(n):
+        ob.set_state(i, holes=int(holes[i]), piece_height=int(height[i]))
+    acts = O.splitmix64_actions(77, 0, steps, n)
+    acts[::4] = 2  # hard drops: every env locks early
+    ref = ob.rollout(acts)
+    big = 0
+    for t in range(steps):
+        act = torch.as_tensor(acts[t], device=a.device)
+        so, sr, sd = a.step(act, obs="packed")
+        uo, ur, ud = unwire(b.step_wire(act), 10, 20)
+        assert torch.equal(uo, so) and torch.equal(ur, sr) and torch.equal(ud, sd), t
+        assert np.array_equal(ur.cpu().numpy(), ref["reward"][t]), t
+        assert np.array_equal(ud.cpu().numpy().astype(np.uint8), ref["done"][t]), t
+        assert np.array_equal(uo.cpu().numpy().view(np.uint32).T, ref["obs"][t]), t
+        big += int((ur.abs() >= 1 << 15).sum())
+    assert big >= n // 2, big  # every env's first lock: |reward| > 2^15
+
+
+@pytest.mark.parametrize("n_global,shards", [(3 * 4096 + 2, 3), (1000, 8), (64, 1)])
+def test_unwire_shards_ragged(n_global, shards):
+    """st_unwire_shards on a gather's receive buffer [shards][words][n_cap]
+    (shard_range's blocks, short shards zero-padded) == st_unwire of the
+    concatenated real columns."""
+    from gym_simpletetris_amd import _lib as C
+    from gym_simpletetris_amd.distributed import shard_cap, shard_range
+    from gym_simpletetris_amd.engine import unwire, unwire_shards
+    W, H = 10, 20
+    words = C.load().st_wire_words(W, H)
+    cap = shard_cap(n_global, shards)
+    g = torch.Generator().manual_seed(n_global)
+    recv = torch.randint(-2**31, 2**31 - 1, (shards, words, cap), dtype=torch.int64, generator=g)
+    recv = recv.to(torch.int32).cuda()
+    cat = torch.cat([recv[r, :, :shard_range(n_global, shards, r)[1]] for r in range(shards)], dim=1).contiguous()
+    eo, er, ed = unwire(cat, W, H)
+    so, sr, sd = unwire_shards(recv, W, H, n_global)
+    assert torch.equal(so, eo) and torch.equal(sr, er) and torch.equal(sd, ed)
 
 
 def test_wire_abi_errors():
