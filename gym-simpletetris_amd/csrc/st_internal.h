@@ -39,7 +39,9 @@ struct KParams {
                         // counter rows read from the first workgroup's lines,
                         // 2048 = lock-path counter stores dropped, 4096 = board
                         // stores dropped, 8192 = late counter loads from the
-                        // first workgroup's lines
+                        // first workgroup's lines, 16384 / 32768 = the logic /
+                        // draw wave's part of 2048 only; 65536 / 131072 = the
+                        // draw wave's count / MT-word store only
     uint64_t *stamps;   // DIAGNOSTIC build only (env ST_STAMPS at st_create): per-wave
                         // s_memtime at 8 phase boundaries of the step kernel
     int32_t k;          // st_rollout: number of steps

@@ -190,6 +190,38 @@ constexpr int kNT = 2;
 // step: K = 2,000 4.67-4.72 -> 4.64-4.67 us, profiles/r03/ab_step_lprio.txt).
 constexpr int kDrawPrio = 2;
 constexpr int kLogicPrio = 1;
+// A/B knobs (round 5, partial-write study): store whole rows instead of the
+// changed 16-B groups / lanes only (same values, full lines written)
+#ifndef ST_FULL_BOARD
+#define ST_FULL_BOARD 0
+#endif
+#ifndef ST_FULL_LCNT
+#define ST_FULL_LCNT 0
+#endif
+#ifndef ST_FULL_DCNT
+#define ST_FULL_DCNT 0
+#endif
+// A/B knob (round 5): st_step's draw wave stores the spawned shape's count
+// right after B1 (known since the step started: the preview's shape) instead
+// of at the end of its chain (same-step auto-reset; lanes without a preview
+// keep the late store)
+#ifndef ST_EARLY_COUNT
+#define ST_EARLY_COUNT 0
+#endif
+// A/B knob (round 5): st_rollout's draw wave keeps each
+// lane's 16-word MT window in LDS (wb[j][lane]) instead of registers: the
+// words at the lane's offset are read by address (ds_read2st64) instead of
+// the 3-stage select network, and a reload is merged by LDS writes instead of
+// 16 register selects
+#ifndef ST_RO_LDSWIN
+#define ST_RO_LDSWIN 0
+#endif
+// A/B knob (round 5): st_step's logic wave stores its lock-path counters, the
+// episode rows of a reset and the clock right after the lock path, before the
+// obs / board store burst, instead of at the end of its chain
+#ifndef ST_EARLY_CNT
+#define ST_EARLY_CNT 0
+#endif
 template <int AUX = 0>
 __device__ __forceinline__ void buf_store16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
     const i32x4 d = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
@@ -751,9 +783,10 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
 // getrandbits(k); lanes they do not settle continue from memory (draw_slow).
 // Same rule as draw_shape (randint(1, sum(m)), tetris_env.py:183-191); `mta`
 // (idx | pg | cur) and `o` advance past the words consumed.  Wave-uniform.
-template <bool FIN_ALL>
+template <bool FIN_ALL, bool LW = false>
 __device__ __forceinline__ int draw_win(bool need, const int32_t (&cnt)[7], uint32_t &mta, const MtPre &wv, int &o,
-                                        int wlim, uint32_t *mt_wave, uint32_t *S, int lane) {
+                                        int wlim, uint32_t *mt_wave, uint32_t *S, int lane,
+                                        const uint32_t *wb = nullptr) {
     int32_t maxc = cnt[0], sumc = cnt[0];
 #pragma unroll
     for (int i = 1; i < 7; ++i) {
@@ -776,15 +809,25 @@ __device__ __forceinline__ int draw_win(bool need, const int32_t (&cnt)[7], uint
         // reloaded after every draw, so o is the previous draw's few words;
         // o >= 8 takes the memory path)
         const int os = o & 7;
-        const uint32_t m4 = 0u - (uint32_t)((os >> 2) & 1), m2 = 0u - (uint32_t)((os >> 1) & 1);
-        const uint32_t m1 = 0u - (uint32_t)(os & 1);
-        uint32_t b[11], c[9], w8[8];
+        uint32_t w8[8];
+        if constexpr (LW) {
+            // the window in LDS, wb[j * 64 + lane]: the 8 words at os by
+            // address (bank = lane whatever the offset; ds_read2st64 pairs)
+            const uint32_t *w0 = wb + os * kWave + lane;
 #pragma unroll
-        for (int j = 0; j < 11; ++j) b[j] = pick(wv.w[j + 4], wv.w[j], m4);
+            for (int j = 0; j < 8; ++j) w8[j] = w0[j * kWave];
+            (void)pick;
+        } else {
+            const uint32_t m4 = 0u - (uint32_t)((os >> 2) & 1), m2 = 0u - (uint32_t)((os >> 1) & 1);
+            const uint32_t m1 = 0u - (uint32_t)(os & 1);
+            uint32_t b[11], c[9];
 #pragma unroll
-        for (int j = 0; j < 9; ++j) c[j] = pick(b[j + 2], b[j], m2);
+            for (int j = 0; j < 11; ++j) b[j] = pick(wv.w[j + 4], wv.w[j], m4);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) w8[j] = pick(c[j + 1], c[j], m1);
+            for (int j = 0; j < 9; ++j) c[j] = pick(b[j + 2], b[j], m2);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w8[j] = pick(c[j + 1], c[j], m1);
+        }
         const int nv = o < 8 ? wlim - o : 0;  // valid words from o
         // words 0-3 tempered as independent chains (acceptance >= 1/2, ~0.7
         // typically: 4 rejections in a row are rare), 4-7 where a lane needs them
@@ -1082,9 +1125,18 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     constexpr bool LCL = KSTEPS == 1 && !VEC;
     // staged counter groups (rows 4q .. 4q + 3): logic 0-1, draw 2-3; with
     // late rows only what the other role still reads early
+    // LCL: the draw wave stages exactly the rows it reads, the shape counts
+    // and the MT word (rows COUNT0 .. MT_INDEX: two 4-row groups from row 6,
+    // a group's base row needs no alignment) -- round 4 staged rows 4..15,
+    // 16 B per env more
+    static_assert(ST_STAT_MT_INDEX == ST_STAT_COUNT0 + 7, "counts and MT word: 8 consecutive rows");
     auto mine_q = [&](int q) {
-        if constexpr (LCL) return ROLE == kRoleD && q >= 1;
+        if constexpr (LCL) return ROLE == kRoleD && (q == 1 || q == 2);
         return (ROLE == kRoleL) == (q < 2);
+    };
+    auto qbase = [&](int q) -> int {  // first stats row of staged group q
+        if constexpr (LCL) return ST_STAT_COUNT0 + 4 * (q - 1);
+        return 4 * q;
     };
     // Rows past the last real row (board padding, counter row 15) re-read the
     // last row -- the same cache line another lane fetches -- instead of
@@ -1106,8 +1158,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
 #pragma unroll
     for (int q = 0; q < kHotQ; ++q)
         if (mine_q(q))
-            sv[q] = *reinterpret_cast<const uint4 *>(ssrc + (size_t)(4 * q) * sd +
-                                                     (4 * q + 4 <= kHotRows ? loff : clamp_off(q, kHotRows)));
+            sv[q] = *reinterpret_cast<const uint4 *>(ssrc + (size_t)qbase(q) * sd +
+                                                     (qbase(q) + 4 <= kHotRows ? loff : clamp_off(q, kHotRows)));
     const int K = KSTEPS ? KSTEPS : p.k;
     // two-wave st_step: the logic wave also builds the next-generation block
     // (the draw wave's chain is the longer one).  (Measured and dropped: the
@@ -1187,7 +1239,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     }
 #pragma unroll
     for (int q = 0; q < kHotQ; ++q)
-        if (mine_q(q)) *reinterpret_cast<uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]) = sv[q];
+        if (mine_q(q)) *reinterpret_cast<uint4 *>(&SS[(qbase(q) + lrow) * kWave + lcc]) = sv[q];
     if constexpr (OVP && DO_L) {
 #pragma unroll
         for (int q = 0; q < NBQ; ++q)
@@ -1286,7 +1338,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
 #pragma unroll
         for (int j = 0; j < 5; ++j)
             lcv[j] = __builtin_amdgcn_raw_buffer_load_b32(
-                rs, locknow ? eo + (uint32_t)(ST_STAT_SCORE + j) * (uint32_t)sd * 4u : kOff, 0, 0);
+                rs, (ST_FULL_LCNT ? real : locknow) ? eo + (uint32_t)(ST_STAT_SCORE + j) * (uint32_t)sd * 4u : kOff,
+                0, 0);
     }
     // the draw wave's next-generation chunk of this step: operands issued
     // before B1, so they arrive while it waits for the lock decision
@@ -1337,6 +1390,17 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     constexpr int kWin = STEP2 ? 8 : 16;
     MtPre pre;
     if constexpr (DO_D) mt_pre_load<kWin>(mrs, mtst, want_pre, pre);
+    // ST_EARLY_COUNT: the spawned shape's count, stored now (after the window
+    // loads are issued) where the spawn takes the preview
+    [[maybe_unused]] const bool early_c = ST_EARLY_COUNT && DO_D && STEP2 && !VEC &&
+                                          p.autoreset == ST_AUTORESET_SAME_STEP;
+    if constexpr (ST_EARLY_COUNT && DO_D && STEP2 && !VEC) {
+        const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
+        __builtin_amdgcn_raw_buffer_store_b32(
+            (uint32_t)csid, rs,
+            early_c && locknow && pv_ok(mt0) ? (uint32_t)e * 4u + (uint32_t)(ST_STAT_COUNT0 + pv_id(mt0)) * (uint32_t)sd * 4u
+                                             : kOff, 0, kNT);
+    }
 
     // ---------------- logic: lock path (tetris_env.py:263-299) ----------------
     bool died = false, spawn = false;
@@ -1498,6 +1562,40 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         __builtin_amdgcn_raw_buffer_store_b32(rew, rr, real ? (uint32_t)e * 4u : kOff, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b8((char)(died ? 1 : 0), rd, real ? (uint32_t)e : kOff, 0, 0);
     }
+    // ECNT: the counters known after the lock path stored now (see ST_EARLY_CNT)
+    constexpr bool ECNT = ST_EARLY_CNT && DO_L && STEP2 && LCL && !VEC;
+    if constexpr (ECNT) {
+        if (locknow) {
+            o_score = (int32_t)lcv[0];
+            o_lines = (int32_t)lcv[1];
+            o_holes = (int32_t)lcv[2];
+            o_height = (int32_t)lcv[3];
+            o_deaths = (int32_t)lcv[4];
+            score += o_score;
+            lines += o_lines;
+            deaths += o_deaths;
+            if (!hset) height = o_height;
+        }
+        const auto rs = buf_rsrc(p.stats, (uint32_t)ST_NSTAT * (uint32_t)sd * 4u);
+        const uint32_t eo = (uint32_t)e * 4u;
+        auto put = [&](int r, int32_t v, bool on) {
+            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, on ? eo + (uint32_t)r * (uint32_t)sd * 4u : kOff,
+                                                  0, kNT);
+        };
+        // the finished episode's counters (ST_AUTORESET_SAME_STEP)
+        put(ST_STAT_EP_TIME, time, reset_now);
+        put(ST_STAT_EP_SCORE, score, reset_now);
+        put(ST_STAT_EP_LINES, lines, reset_now);
+        put(ST_STAT_EP_HOLES, holes, reset_now);
+        if (reset_now) time = score = lines = holes = height = 0;
+        const bool cst = !(kAblate & (2048u | 16384u));
+        put(ST_STAT_TIME, time, true);
+        put(ST_STAT_SCORE, score, cst && locknow && score != o_score);
+        put(ST_STAT_LINES, lines, cst && locknow && lines != o_lines);
+        put(ST_STAT_HOLES, holes, cst && locknow && holes != o_holes);
+        put(ST_STAT_PIECE_HEIGHT, height, cst && locknow && height != o_height);
+        put(ST_STAT_DEATHS, deaths, cst && locknow && deaths != o_deaths);
+    }
     if constexpr (DO_L && KSTEPS == 1) {
         // The post-step board never depends on the spawned piece either (a
         // spawn only overlays row 0, which is empty after a non-fatal lock,
@@ -1590,7 +1688,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 v.z &= km.z;
                 v.w &= km.w;
                 // row 4q + lrow; padding rows (>= W) are never dirty
-                const bool dirty = (bdl >> (4 * q)) & 1u && 4 * q + lrow < W && !(kAblate & 4096u);
+                const bool dirty = (ST_FULL_BOARD || ((bdl >> (4 * q)) & 1u)) && 4 * q + lrow < W && !(kAblate & 4096u);
                 buf_store16<kNT>(rb, dirty ? boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff, v);
             }
         }
@@ -1674,11 +1772,22 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
             const uint32_t eo = (uint32_t)e * 4u;
             // (ablation 2048: the lock-path counter stores dropped, timing only)
-            const bool cst = !(kAblate & 2048u);
+            const bool cst = !(kAblate & (2048u | 32768u));
+            if constexpr (ST_FULL_DCNT && !VEC) {  // (A/B: every lane stores the count rows and the MT word)
+                __builtin_amdgcn_raw_buffer_store_b32(
+                    mt_out, rs, cst && real ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff, 0, kNT);
+#pragma unroll
+                for (int i = 0; i < 7; ++i)
+                    __builtin_amdgcn_raw_buffer_store_b32(
+                        dr && i == sid ? (uint32_t)csid : ss(ST_STAT_COUNT0 + i), rs,
+                        cst && real ? eo + (uint32_t)(ST_STAT_COUNT0 + i) * (uint32_t)sd * 4u : kOff, 0, kNT);
+            } else {
             __builtin_amdgcn_raw_buffer_store_b32(
-                mt_out, rs, cst && (dr || chunk_me) ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff, 0, kNT);
+                mt_out, rs, cst && !(kAblate & 131072u) && (dr || chunk_me) ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff, 0, kNT);
             __builtin_amdgcn_raw_buffer_store_b32(
-                (uint32_t)csid, rs, cst && dr ? eo + (uint32_t)(ST_STAT_COUNT0 + sid) * (uint32_t)sd * 4u : kOff, 0, kNT);
+                (uint32_t)csid, rs, cst && !(kAblate & 65536u) && dr && !(early_c && pv_ok(mt0))
+                                        ? eo + (uint32_t)(ST_STAT_COUNT0 + sid) * (uint32_t)sd * 4u : kOff, 0, kNT);
+            }
             if constexpr (VEC) {  // st_step_vec's info snapshot: the shape counts after the step
                 const auto ri = buf_rsrc(p.info, (uint32_t)ST_NSTAT * (uint32_t)p.n * 4u);
 #pragma unroll
@@ -1713,10 +1822,10 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         }
 
         // ---- counters back to the staged rows (tetris_env.py:253, :264-299) ----
-        if constexpr (LCL) {
+        if constexpr (LCL && !ECNT) {
             // the late-loaded counters (issued before B1; the lock path kept
             // deltas) -- absolute values and the old ones for the dirty tests
-            if (locknow) {
+            if (ST_FULL_LCNT || locknow) {
                 o_score = (int32_t)lcv[0];
                 o_lines = (int32_t)lcv[1];
                 o_holes = (int32_t)lcv[2];
@@ -1737,7 +1846,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 ep_h = holes;
             }
         }
-        if (reset_now) {  // the finished episode's counters (ST_AUTORESET_SAME_STEP)
+        if (!ECNT && reset_now) {  // the finished episode's counters (ST_AUTORESET_SAME_STEP)
             int32_t *st = p.stats + e;
             st[ST_STAT_EP_TIME * sd] = time;
             st[ST_STAT_EP_SCORE * sd] = score;
@@ -1757,14 +1866,15 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, on ? eo + (uint32_t)r * (uint32_t)sd * 4u : kOff,
                                                       0, kNT);
             };
-            put(ST_STAT_TIME, time, true);
+            if constexpr (!ECNT) put(ST_STAT_TIME, time, true);
             put(kPieceRow, (int32_t)pw_out, true);
-            const bool cst = !(kAblate & 2048u);  // (ablation: lock-path counter stores dropped)
-            put(ST_STAT_SCORE, score, cst && locknow && score != o_score);
-            put(ST_STAT_LINES, lines, cst && locknow && lines != o_lines);
-            put(ST_STAT_HOLES, holes, cst && locknow && holes != o_holes);
-            put(ST_STAT_PIECE_HEIGHT, height, cst && locknow && height != o_height);
-            put(ST_STAT_DEATHS, deaths, cst && locknow && deaths != o_deaths);
+            const bool cst = !ECNT && !(kAblate & (2048u | 16384u));  // (ablation: lock-path counter stores dropped)
+            const bool fl = ST_FULL_LCNT && LCL && real;  // (A/B: every lane stores every row)
+            put(ST_STAT_SCORE, score, cst && (fl || (locknow && score != o_score)));
+            put(ST_STAT_LINES, lines, cst && (fl || (locknow && lines != o_lines)));
+            put(ST_STAT_HOLES, holes, cst && (fl || (locknow && holes != o_holes)));
+            put(ST_STAT_PIECE_HEIGHT, height, cst && (fl || (locknow && height != o_height)));
+            put(ST_STAT_DEATHS, deaths, cst && (fl || (locknow && deaths != o_deaths)));
             if constexpr (VEC) {
                 // st_step_vec's info snapshot: this wave's rows for every env
                 // (locking lanes from the registers, the others unchanged)
@@ -2094,6 +2204,7 @@ struct RoLds {
     // packed obs (the output wave builds the next-generation chunks):
     uint32_t cw[kWave];   // per lane: chunk candidate << 31 | cur << 10 | pg (draw -> output)
     uint32_t cpg[kWave];  // per lane: valid << 31 | cur << 10 | pg after a chunk (output -> draw)
+    uint32_t wb[ST_RO_LDSWIN ? kMtWin * kWave : 1];  // ST_RO_LDSWIN: the draw wave's MT windows [j][lane]
     uint32_t fl, fd, fo, fq;  // progress counters (see above)
 };
 // d[r] by selects on values (a select between two array elements would be
@@ -2627,6 +2738,11 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
         int o = 0, wlim = win_lim(mta), o_rl = 0, wlim_n = 0;
         mt_pre_load<kMtWin>(mrs, mta, real, win);
         mt_win_consume<kMtWin>(win);
+        constexpr bool LW = ST_RO_LDSWIN;
+        if constexpr (LW) {
+#pragma unroll
+            for (int j = 0; j < kMtWin; ++j) sm.wb[j * kWave + lane] = win.w[j];
+        }
         int q0 = pv_id(w0), q1;
         {
             // the queue's two pieces: q0 where the state has no preview
@@ -2634,14 +2750,14 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             // counts after q0's spawn
             const bool need1 = real && !pv_ok(w0);
             if (__ballot(need1)) {
-                const int pk = draw_win<CHO>(need1, cnt_r, mta, win, o, wlim, mtg, sm.S, lane);
+                const int pk = draw_win<CHO, LW>(need1, cnt_r, mta, win, o, wlim, mtg, sm.S, lane, sm.wb);
                 if (need1) q0 = pk;
             }
             int32_t cq[7];
 #pragma unroll
             for (int i = 0; i < 7; ++i) cq[i] = cnt_r[i] + (i == q0);
             const uint32_t m0 = mta;
-            q1 = draw_win<CHO>(real, cq, mta, win, o, wlim, mtg, sm.S, lane);
+            q1 = draw_win<CHO, LW>(real, cq, mta, win, o, wlim, mtg, sm.S, lane, sm.wb);
             c1 = mt_consumed(m0, mta);
         }
         int32_t cq[7];  // shape counts once the queue's head has spawned
@@ -2711,7 +2827,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 for (int i = 0; i < 7; ++i) cq[i] += (int32_t)((oh >> i) & 1u);
             }
             const uint32_t m0 = mta;
-            const int pk = draw_win<CHO>(cons, cq, mta, win, o, wlim, mtg, sm.S, lane);
+            const int pk = draw_win<CHO, LW>(cons, cq, mta, win, o, wlim, mtg, sm.S, lane, sm.wb);
             stamp(5);
             if (cons) {
                 q1 = pk;
@@ -2749,7 +2865,10 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             stamp(7);
             if (rl) {
 #pragma unroll
-                for (int j = 0; j < kMtWin; ++j) win.w[j] = wn.w[j];
+                for (int j = 0; j < kMtWin; ++j) {
+                    if constexpr (LW) sm.wb[j * kWave + lane] = wn.w[j];
+                    else win.w[j] = wn.w[j];
+                }
                 o -= o_rl;
                 wlim = wlim_n;
             }
