@@ -67,7 +67,7 @@ def test_library_is_the_hip_build():
     G = _engine()
     from gym_simpletetris_amd import _lib
     L = _lib.load()
-    assert L.st_abi_version() == C.ABI_VERSION
+    assert L.st_abi_version() == _lib.ABI_VERSION
     b = G.TetrisBatch(3, seeds=[1, 2, 3])
     b.reset()
     b.step(np.zeros(3, np.uint8))
@@ -877,7 +877,7 @@ def test_mt_generations_across_steps():
         raw = torch.empty(b.stride, dtype=torch.int32, device=b.device)
         v = b._views
         C.check(b._L.st_copy(ctypes.c_void_p(raw.data_ptr()),
-                             ctypes.c_void_p(v.stats + C.STAT["mt_index"] * v.stride * 4),
+                             ctypes.c_void_p(v.hot + C.HOT["mt"] * v.stride * 4),
                              raw.numel() * 4, b._stream()))
         saw_lazy |= bool((((raw[:n].cpu().numpy() >> 20) & 1) != 0).any())   # current generation in B
         if (c0 // chunk) % 3 == 1:
@@ -971,7 +971,7 @@ def test_preview_rewind_across_generations():
         assert np.array_equal(r.cpu().numpy(), ref["reward"][0]), t
         assert np.array_equal(o.cpu().numpy().view(np.uint32).T, ref["obs"][0]), t
         C.check(b._L.st_copy(ctypes.c_void_p(raw.data_ptr()),
-                             ctypes.c_void_p(v.stats + C.STAT["mt_index"] * v.stride * 4),
+                             ctypes.c_void_p(v.hot + C.HOT["mt"] * v.stride * 4),
                              raw.numel() * 4, b._stream()))
         w = raw[:n].cpu().numpy().astype(np.uint32)
         ok = ((w >> 24) & 1).astype(bool)

@@ -9,7 +9,9 @@ wall time, HIP-event span.  Modes (interleaved, REPS each):
   nosum     without the spawned-count reduction (torch ops) before it
   noev      without the event record right before the first launch
   bare      synchronize, K launches, synchronize (no torch ops, no events)
-One JSON line per region."""
+With PRELUDES=1 the bare region after one operation each: a device
+allocation of a new size (hipMalloc), of a cached size, a device->host
+read (.item()), a device copy, a torch kernel.  One JSON line per region."""
 import ctypes
 import json
 import os
@@ -48,8 +50,28 @@ def spawned():
     return st.to(torch.int64).sum()
 
 
+scratch = torch.zeros(7, dtype=torch.int64, device=dev)
+grow = [1 << 20]
+
+
+def prelude(mode):
+    """Extra preludes (PRELUDES=1): one operation, then the bare region."""
+    if mode == "alloc":  # a never-seen size: the caching allocator calls hipMalloc
+        grow[0] += 4096
+        torch.empty(grow[0], dtype=torch.uint8, device=dev)
+    elif mode == "alloc_cached":  # a size freed before: no hipMalloc
+        torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+    elif mode == "item":  # a device->host read
+        scratch[0].item()
+    elif mode == "d2d":  # a device copy on the stream
+        C.check(L.st_copy(ctypes.c_void_p(scratch.data_ptr()), ctypes.c_void_p(scratch.data_ptr() + 8), 8, sp))
+    elif mode == "torch_kernel":  # a torch kernel on the stream
+        scratch.add_(1)
+
+
 def region(mode, t0):
     with torch.cuda.stream(s):
+        prelude(mode)
         if mode in ("bench", "noev"):
             spawned()
         if mode != "bare":
@@ -80,8 +102,11 @@ with torch.cuda.stream(s):
         fn(*args[t])
 torch.cuda.synchronize()
 t0 = 5
+MODES = ("bench", "nosum", "noev", "bare")
+if os.environ.get("PRELUDES"):
+    MODES = ("bare", "alloc", "alloc_cached", "item", "d2d", "torch_kernel")
 for rep in range(REPS):
-    for mode in ("bench", "nosum", "noev", "bare"):
+    for mode in MODES:
         r = region(mode, t0)
         t0 = (t0 + K) % (T - K)
         r["rep"] = rep
