@@ -687,7 +687,8 @@ __device__ __forceinline__ uint32_t dw_from_counts(const int32_t (&c)[7]) {
 // (counts[s] += 1: _new_piece, tetris_env.py:199) -- the preview draw's
 // parameters before anything but the hot words is known.  `ok` false: the
 // word was escaped or a distance would pass 15 (the full counts decide).
-__device__ __forceinline__ DrawPar draw_par_dw(uint32_t dw, int s, bool &ok) {
+// `wn`: the draw word after the spawn (valid where `ok`).
+__device__ __forceinline__ DrawPar draw_par_dw(uint32_t dw, int s, bool &ok, uint32_t &wn) {
     const uint32_t sh = 4u * (uint32_t)s;
     const uint32_t ds = (dw >> sh) & 15u;
     // s at the maximum: it becomes the sole maximum, every other distance
@@ -696,6 +697,7 @@ __device__ __forceinline__ DrawPar draw_par_dw(uint32_t dw, int s, bool &ok) {
     const bool has15 = ((x - 0x1111111u) & ~x & 0x8888888u) != 0u;
     ok = !(dw & kDwEsc) && !(ds == 0u && has15);
     const uint32_t w = ds ? dw - (1u << sh) : (dw & 0xFFFFFFFu) + 0x1111111u - (1u << sh);
+    wn = w;
     DrawPar d;
     int32_t sum = 0;
 #pragma unroll
@@ -1430,7 +1432,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     ST_STAMP(2);
     // LC: the logic wave's lock-path counters, per locking lane (an
     // out-of-range offset elsewhere: no traffic, 0)
-    [[maybe_unused]] uint32_t lcv[5] = {};
+    [[maybe_unused]] uint32_t lcv[8] = {};
     if constexpr (LCL && DO_L) {
         // the cold record's first 20 B (score, lines, holes, piece_height,
         // deaths: one 32-B sector of the env's 64-B record)
@@ -1442,7 +1444,15 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         lcv[1] = l4.y;
         lcv[2] = l4.z;
         lcv[3] = l4.w;
+#if ST_COLD_FULL
+        const u32x4 l4b = __builtin_amdgcn_raw_buffer_load_b128(rc, locknow ? eo + 16u : kOff, 0, 0);
+        lcv[4] = l4b.x;
+        lcv[5] = l4b.y;
+        lcv[6] = l4b.z;
+        lcv[7] = l4b.w;
+#else
         lcv[4] = __builtin_amdgcn_raw_buffer_load_b32(rc, locknow ? eo + (uint32_t)kCDeaths * 4u : kOff, 0, 0);
+#endif
     }
     // the draw wave's next-generation chunk of this step: operands issued
     // before B1, so they arrive while it waits for the lock decision
@@ -1456,15 +1466,16 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     [[maybe_unused]] DrawPar dpar;
     [[maybe_unused]] int32_t csid = 0;  // the spawned shape's count after the spawn
     [[maybe_unused]] bool dw_ok = true;   // LCL: dpar from the draw word is valid
+    [[maybe_unused]] uint32_t dwn = 0;    // LCL: the draw word after the spawn
     if constexpr (DO_D) {
         mrs = mt_res(p.mt + e0 * kMtPitch, lane);
         mt_chunk_issue(mrs, mt0, real && !(kAblate & 2u), lane, chunk);
         const int s0 = pv_id(mt0);
         if constexpr (LCL) {
-            // from the draw word (the counts are read after B1, per locking
-            // lane): the counts after the preview spawns; dw_ok false (an
+            // from the draw word (the counts are read only on the rare
+            // paths): the counts after the preview spawns; dw_ok false (an
             // escaped word, p ~ 1e-5 per draw): recomputed from the counts
-            dpar = draw_par_dw(ss(kSsDraw), s0, dw_ok);
+            dpar = draw_par_dw(ss(kSsDraw), s0, dw_ok, dwn);
         } else {
 #pragma unroll
             for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)ss(ST_STAT_COUNT0 + i) + (i == s0);  // _new_piece :199
@@ -1501,14 +1512,13 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     constexpr int kWin = STEP2 ? 8 : 16;
     MtPre pre;
     if constexpr (DO_D) mt_pre_load<kWin>(mrs, mtst, want_pre, pre);
-    // LCL: the locking lanes' shape counts, the second 32-B sector of the
-    // cold record (words 8..15: ep_holes, counts), issued with the window
-    [[maybe_unused]] u32x4 cc0, cc1;
+    // LCL: the preview shape's count (one cold word per locking lane, issued
+    // with the window, consumed only at the commit): its count after the spawn
+    [[maybe_unused]] uint32_t cs0 = 0;
     if constexpr (LCL && DO_D) {
         const auto rc = buf_rsrc(p.cold, (uint32_t)sd * (uint32_t)kCold * 4u);
-        const uint32_t co = (uint32_t)e * (uint32_t)(kCold * 4) + 32u;
-        cc0 = __builtin_amdgcn_raw_buffer_load_b128(rc, want_pre ? co : kOff, 0, 0);
-        cc1 = __builtin_amdgcn_raw_buffer_load_b128(rc, want_pre ? co + 16u : kOff, 0, 0);
+        const uint32_t co = (uint32_t)e * (uint32_t)(kCold * 4) + (uint32_t)(kCCount0 + pv_id(mt0)) * 4u;
+        cs0 = __builtin_amdgcn_raw_buffer_load_b32(rc, want_pre ? co : kOff, 0, 0);
     }
 
     // ---------------- logic: lock path (tetris_env.py:263-299) ----------------
@@ -1787,30 +1797,36 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         uint32_t mt_new = mtst;
         if (!(kAblate & 2u)) {
             mt_win_consume<kWin>(pre);
-            // LCL: the locking lanes' counts (cold words 9..15, loaded with
-            // the window): the spawned shape's count, the new draw word and
-            // the rare fallbacks below
+            // LCL: all counts (cold words 9..15) only for the rare lanes --
+            // an escaped draw word, or no preview -- whose draws they
+            // decide; the common spawn needs only its shape's count (cs0)
             [[maybe_unused]] int32_t cf[7] = {};
+            const bool need1 = dr_spec && !pv_ok(mt0);
             if constexpr (LCL) {
-                const int s0 = pv_id(mt0);
-                cf[0] = (int32_t)cc0.y;
-                cf[1] = (int32_t)cc0.z;
-                cf[2] = (int32_t)cc0.w;
-                cf[3] = (int32_t)cc1.x;
-                cf[4] = (int32_t)cc1.y;
-                cf[5] = (int32_t)cc1.z;
-                cf[6] = (int32_t)cc1.w;
+                const bool rare = dr_spec && (!dw_ok || need1);
+                if (__ballot(rare)) {
+                    const auto rc = buf_rsrc(p.cold, (uint32_t)sd * (uint32_t)kCold * 4u);
+                    const uint32_t co = (uint32_t)e * (uint32_t)(kCold * 4) + 32u;
+                    const u32x4 cc0 = __builtin_amdgcn_raw_buffer_load_b128(rc, rare ? co : kOff, 0, 0);
+                    const u32x4 cc1 = __builtin_amdgcn_raw_buffer_load_b128(rc, rare ? co + 16u : kOff, 0, 0);
+                    cf[0] = (int32_t)cc0.y;
+                    cf[1] = (int32_t)cc0.z;
+                    cf[2] = (int32_t)cc0.w;
+                    cf[3] = (int32_t)cc1.x;
+                    cf[4] = (int32_t)cc1.y;
+                    cf[5] = (int32_t)cc1.z;
+                    cf[6] = (int32_t)cc1.w;
+                    const int s0 = pv_id(mt0);
 #pragma unroll
-                for (int i = 0; i < 7; ++i) cnt[i] = cf[i] + (i == s0);  // _new_piece :199
-                csid = cnt[0];
-#pragma unroll
-                for (int i = 1; i < 7; ++i) csid = s0 == i ? cnt[i] : csid;
-                if (__ballot(dr_spec && !dw_ok)) {  // an escaped draw word: the counts decide
+                    for (int i = 0; i < 7; ++i) cnt[i] = cf[i] + (i == s0);  // _new_piece :199
                     const DrawPar d2 = draw_par(cnt);
-                    if (!dw_ok) dpar = d2;
+                    const uint32_t w2 = dw_from_counts(cnt);
+                    if (!dw_ok) {  // an escaped draw word: the counts decide
+                        dpar = d2;
+                        dwn = w2;
+                    }
                 }
             }
-            const bool need1 = dr_spec && !pv_ok(mt0);
             if (__ballot(need1)) {  // rare: after st_seed / st_mt_sync / a host-written state
                 // the piece first, with the counts before the spawn
                 int32_t c0[7];
@@ -1824,7 +1840,16 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
 #pragma unroll
                     for (int i = 0; i < 7; ++i) csid = pk == i ? cnt[i] : csid;
                 }
-                dpar = draw_par(cnt);
+                const DrawPar d1 = draw_par(cnt);
+                if constexpr (LCL) {
+                    const uint32_t w1 = dw_from_counts(cnt);
+                    if (need1) {
+                        dpar = d1;
+                        dwn = w1;
+                    }
+                } else {
+                    dpar = d1;
+                }
             }
             sm.pick1[lane] = (uint32_t)sid;
             if (lane == 0) lds_flag_set(&sm.f2, (uint32_t)t + 1u);
@@ -1877,8 +1902,11 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             __builtin_amdgcn_raw_buffer_store_b32(
                 mt_out, rh, cst && !(kAblate & 131072u) && (dr || chunk_me) ? eo + (uint32_t)kHotMt * (uint32_t)sd * 4u : kOff,
                 0, kNT);
-            __builtin_amdgcn_raw_buffer_store_b32(
-                dw_from_counts(cnt), rh, cst && dr ? eo + (uint32_t)kHotDraw * (uint32_t)sd * 4u : kOff, 0, kNT);
+            __builtin_amdgcn_raw_buffer_store_b32(LCL ? dwn : dw_from_counts(cnt), rh,
+                                                  cst && dr ? eo + (uint32_t)kHotDraw * (uint32_t)sd * 4u : kOff, 0, kNT);
+            // (LCL: shape_counts[name] += 1, :199, from the preview's count
+            // word; a lane that drew its piece first counted it above)
+            if constexpr (LCL) csid = pv_ok(mt0) ? (int32_t)cs0 + 1 : csid;
             __builtin_amdgcn_raw_buffer_store_b32(
                 (uint32_t)csid, rc, cst && !(kAblate & 65536u) && dr ? ec + (uint32_t)(kCCount0 + sid) * 4u : kOff, 0, kNT);
             if constexpr (VEC) {  // st_step_vec's info snapshot: the shape counts after the step
@@ -1939,8 +1967,10 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 ep_h = holes;
             }
         }
-        // the finished episode's counters (ST_AUTORESET_SAME_STEP): cold words 5..8
-        store_ep(p, e, time, score, lines, holes, reset_now);
+        // the finished episode's counters (ST_AUTORESET_SAME_STEP): cold words
+        // 5..8 (st_step: with the deaths word below, two stores)
+        [[maybe_unused]] const int32_t x_t = time, x_s = score, x_l = lines, x_h = holes;
+        if constexpr (!LCL) store_ep(p, e, time, score, lines, holes, reset_now);
         if (reset_now) time = score = lines = holes = height = 0;
         // st_step stores only the counter rows that changed (per env)
         if constexpr (STEP2) {
@@ -1964,11 +1994,46 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             put(ST_STAT_TIME, time, true);
             put(kPieceRow, (int32_t)pw_out, true);
             const bool cst = !(kAblate & (2048u | 16384u));  // (ablation: lock-path counter stores dropped)
-            put(ST_STAT_SCORE, score, cst && locknow && score != o_score);
-            put(ST_STAT_LINES, lines, cst && locknow && lines != o_lines);
-            put(ST_STAT_HOLES, holes, cst && locknow && holes != o_holes);
-            put(ST_STAT_PIECE_HEIGHT, height, cst && locknow && height != o_height);
-            put(ST_STAT_DEATHS, deaths, cst && locknow && deaths != o_deaths);
+            if constexpr (LCL) {
+                // the cold record's words 0..8 in at most three stores per
+                // lane (one 64-B record: a store per word would cost the
+                // memory pipeline a record's segment per instruction):
+                // words 0..3 where one of them changed; a same-step reset's
+                // words 4..7 (deaths, ep_time, ep_score, ep_lines) and 8
+                // (ep_holes); else the deaths word where a death counted
+                const bool c4 = locknow && (score != o_score || lines != o_lines || holes != o_holes || height != o_height);
+                u32x4 v4 = {(uint32_t)score, (uint32_t)lines, (uint32_t)holes, (uint32_t)height};
+#if ST_COLD_FULL
+                // (variant: whole 32-B sectors -- words 0..7 rewritten as loaded
+                // where anything in them changed)
+                const bool c8 = c4 || (locknow && deaths != o_deaths);
+                u32x4 w4 = {(uint32_t)deaths, reset_now ? (uint32_t)x_t : lcv[5], reset_now ? (uint32_t)x_s : lcv[6],
+                            reset_now ? (uint32_t)x_l : lcv[7]};
+                __builtin_amdgcn_raw_buffer_store_b128(v4, rc, cst && c8 ? ec : kOff, 0, kNT);
+                __builtin_amdgcn_raw_buffer_store_b128(w4, rc, cst && c8 ? ec + 16u : kOff, 0, kNT);
+                __builtin_amdgcn_raw_buffer_store_b32((uint32_t)x_h, rc, reset_now ? ec + (uint32_t)kCEpHoles * 4u : kOff, 0,
+                                                      kNT);
+                if constexpr (false)
+#endif
+                {
+                __builtin_amdgcn_raw_buffer_store_b128(v4, rc, cst && c4 ? ec : kOff, 0, kNT);
+                if (__ballot(reset_now)) {
+                    u32x4 e4 = {(uint32_t)deaths, (uint32_t)x_t, (uint32_t)x_s, (uint32_t)x_l};
+                    __builtin_amdgcn_raw_buffer_store_b128(e4, rc, reset_now ? ec + (uint32_t)kCDeaths * 4u : kOff, 0, kNT);
+                    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)x_h, rc, reset_now ? ec + (uint32_t)kCEpHoles * 4u : kOff,
+                                                          0, kNT);
+                }
+                __builtin_amdgcn_raw_buffer_store_b32(
+                    (uint32_t)deaths, rc, cst && !reset_now && locknow && deaths != o_deaths ? ec + (uint32_t)kCDeaths * 4u : kOff,
+                    0, kNT);
+                }
+            } else {
+                put(ST_STAT_SCORE, score, cst && locknow && score != o_score);
+                put(ST_STAT_LINES, lines, cst && locknow && lines != o_lines);
+                put(ST_STAT_HOLES, holes, cst && locknow && holes != o_holes);
+                put(ST_STAT_PIECE_HEIGHT, height, cst && locknow && height != o_height);
+                put(ST_STAT_DEATHS, deaths, cst && locknow && deaths != o_deaths);
+            }
             if constexpr (VEC) {
                 // st_step_vec's info snapshot: this wave's rows for every env
                 // (locking lanes from the registers, the others unchanged)

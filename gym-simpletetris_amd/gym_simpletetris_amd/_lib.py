@@ -128,8 +128,13 @@ def load(path: str = LIB_PATH):
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
-    if L.st_abi_version() != ABI_VERSION and not ab_override:
-        raise ImportError(f"libsimpletetris ABI {L.st_abi_version()} != {ABI_VERSION}")
+    if L.st_abi_version() != ABI_VERSION:
+        if not ab_override:
+            raise ImportError(f"libsimpletetris ABI {L.st_abi_version()} != {ABI_VERSION}")
+        # the state-view struct differs across ABIs: an older build serves
+        # raw ctypes A/Bs only (views read through the wrong struct size
+        # tensors from garbage)
+        L.st_state = None
     _lib = L
     return L
 

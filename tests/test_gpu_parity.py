@@ -1248,7 +1248,10 @@ def test_host_written_large_shape_counts(mode):
     (tetris_env.py:183-191; Lib/random.py _randbelow).  The rollout's draw
     skips the tempering's last step only in waves whose lanes all draw <= 18
     bits: one wave here has none of the wide lanes, one only wide lanes, two
-    a mix.  Outputs and final counts / MT index vs the oracle."""
+    a mix.  The first wave's counts spread 14..17 apart: st_step's draw word
+    (nibble distances to the maximum, escaped past 15) crosses its escape
+    boundary both ways as shapes spawn.  Outputs and final counts / MT index
+    vs the oracle."""
     G = _engine()
     n, T = 256, 80
     b = G.TetrisBatch(n, autoreset="same_step", seeds=range(n))
@@ -1259,7 +1262,9 @@ def test_host_written_large_shape_counts(mode):
     mt, stats = st["mt"].copy(), st["stats"].copy()
     rng = np.random.default_rng(23)
     for i in range(n):
-        if 64 <= i < 128:
+        if i < 64:
+            counts = 50 + rng.integers(0, 18, 7)
+        elif 64 <= i < 128:
             counts = np.array([100_000 + 1_000 * i, 0, 0, 0, 0, 0, 0])
         elif i >= 128 and i % 2:
             counts = rng.integers(0, 3_000_000, 7)
