@@ -352,11 +352,12 @@ def main():
         region_probe_*.jsonl)."""
         bufs = pl_bufs.get(id(eng))
         if bufs is None:
-            bufs = pl_bufs[id(eng)] = (torch.empty((C.NSTAT, eng.stride), dtype=torch.int32, device=dev),
+            bufs = pl_bufs[id(eng)] = (torch.empty((7, eng.stride), dtype=torch.int32, device=dev),
                                        torch.zeros(2, dtype=torch.int64, device=dev))
-        st, res = bufs
-        C.check(eng._L.st_get_stats(eng._ctx, ctypes.c_void_p(st.data_ptr()), sp))  # the ST_STAT_* rows
-        torch.sum(st[C.STAT["count0"]:C.STAT["count0"] + 7, :eng.n], dim=(0, 1), dtype=torch.int64, out=res[slot])
+        cnt, res = bufs
+        src = eng._views.stats + C.STAT["count0"] * eng.stride * 4  # rows count0 .. count0 + 6
+        C.check(eng._L.st_copy(ctypes.c_void_p(cnt.data_ptr()), ctypes.c_void_p(src), cnt.numel() * 4, sp))
+        torch.sum(cnt[:, :eng.n], dim=(0, 1), dtype=torch.int64, out=res[slot])
         return res[slot]
 
     def timed(eng, run, nsteps):

@@ -19,8 +19,8 @@ struct st_ctx {
     bool seeded;
     bool reset_once;
     uint32_t *board;
-    uint32_t *hot;   // [kNHot][stride]
-    int32_t *cold;   // [stride][kCold]
+    uint32_t *piece;
+    int32_t *stats;
     uint32_t *mt;
     uint32_t *act_flag;  // st_set_action_flag (caller-owned), or null
     int cus;             // compute units of the device
@@ -74,9 +74,8 @@ st::KParams params(const st_ctx *c) {
     p.n = c->n;
     p.stride = c->stride;
     p.board = c->board;
-    p.hot = c->hot;
-    p.piece = c->hot + (size_t)st::kHotPiece * (size_t)c->stride;
-    p.cold = c->cold;
+    p.piece = c->piece;
+    p.stats = c->stats;
     p.mt = c->mt;
     p.act_flag = c->act_flag;
     p.cus = c->cus;
@@ -85,13 +84,12 @@ st::KParams params(const st_ctx *c) {
 
 void free_state(st_ctx *c) {
     if (c->board) (void)hipFree(c->board);
-    if (c->hot) (void)hipFree(c->hot);
-    if (c->cold) (void)hipFree(c->cold);
+    if (c->stats) (void)hipFree(c->stats);
     if (c->mt) (void)hipFree(c->mt);
     if (c->stamps) (void)hipFree(c->stamps);
     c->stamps = nullptr;
-    c->board = c->hot = c->mt = nullptr;
-    c->cold = nullptr;
+    c->board = c->piece = c->mt = nullptr;
+    c->stats = nullptr;
 }
 
 }  // namespace
@@ -133,8 +131,8 @@ int st_create(st_ctx **out, const st_config *cfg, int device, int64_t n_envs) {
     // board rows padded to a multiple of 4: a wave's 16-B accesses cover 4 rows
     const size_t wpad = (size_t)((cfg->width + 3) & ~3);
     if (e == hipSuccess) e = hipMalloc(&c->board, sd * wpad * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMalloc(&c->hot, sd * st::kNHot * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMalloc(&c->cold, sd * st::kCold * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(&c->stats, sd * ST_NSTAT * sizeof(int32_t));
+    if (e == hipSuccess) c->piece = reinterpret_cast<uint32_t *>(c->stats) + ST_STAT_PIECE * sd;
     // MT states: [stride][kMtPitch] (+ the back pad a draw window may reach)
     if (e == hipSuccess) e = hipMalloc(&c->mt, (sd * st::kMtPitch + st::kMtPadBack) * sizeof(uint32_t));
     // diagnostic phase stamps (ST_STAMPS set: the instrumented step kernel)
@@ -352,29 +350,14 @@ int st_copy(void *dst, const void *src, int64_t bytes, st_stream stream) {
 int st_state(st_ctx *c, st_state_views *out) {
     if (!c || !out) return fail(ST_EINVAL, "st_state: null argument");
     out->board = c->board;
-    out->piece = c->hot + (size_t)st::kHotPiece * (size_t)c->stride;
-    out->hot = c->hot;
-    out->cold = c->cold;
+    out->piece = c->piece;
+    out->stats = c->stats;
     out->mt = c->mt;
     out->mt_pitch = st::kMtPitch;
     out->n_envs = c->n;
     out->stride = c->stride;
     out->width = c->cfg.width;
     out->height = c->cfg.height;
-    return ST_OK;
-}
-
-int st_get_stats(st_ctx *c, int32_t *d_out, st_stream stream) {
-    if (!c || !d_out) return fail(ST_EINVAL, "st_get_stats: null argument");
-    DeviceGuard g(c->device);
-    ST_HIP(st::launch_get_stats(params(c), d_out, (hipStream_t)stream));
-    return ST_OK;
-}
-
-int st_set_stats(st_ctx *c, const int32_t *d_in, st_stream stream) {
-    if (!c || !d_in) return fail(ST_EINVAL, "st_set_stats: null argument");
-    DeviceGuard g(c->device);
-    ST_HIP(st::launch_set_stats(params(c), d_in, (hipStream_t)stream));
     return ST_OK;
 }
 
@@ -422,15 +405,7 @@ int st_save(st_ctx *c, void *host_out, int64_t bytes) {
     ST_HIP(hipDeviceSynchronize());
     ST_HIP(hipMemcpy2D(o, row, c->board, pitch, row, c->cfg.width, hipMemcpyDeviceToHost));
     o += row * c->cfg.width;
-    {  // the canonical ST_STAT_* rows, gathered from the hot rows and cold records
-        int32_t *tmp = nullptr;
-        ST_HIP(hipMalloc(&tmp, pitch * ST_NSTAT));
-        hipError_t e = st::launch_get_stats(params(c), tmp, nullptr);
-        if (e == hipSuccess) e = hipDeviceSynchronize();
-        if (e == hipSuccess) e = hipMemcpy2D(o, row, tmp, pitch, row, ST_NSTAT, hipMemcpyDeviceToHost);
-        (void)hipFree(tmp);
-        if (e != hipSuccess) return hip_fail(e, "st_save: counters");
-    }
+    ST_HIP(hipMemcpy2D(o, row, c->stats, pitch, row, ST_NSTAT, hipMemcpyDeviceToHost));
     o += row * ST_NSTAT;
     const size_t mrow = (size_t)st::kMtN * 4, mpitch = (size_t)st::kMtPitch * 4;
     ST_HIP(hipMemcpy2D(o, mrow, c->mt, mpitch, mrow, (size_t)c->n, hipMemcpyDeviceToHost));
@@ -463,18 +438,7 @@ int st_load(st_ctx *c, const void *host_in, int64_t bytes) {
     ST_HIP(hipDeviceSynchronize());
     ST_HIP(hipMemcpy2D(c->board, pitch, in, row, row, c->cfg.width, hipMemcpyHostToDevice));
     in += row * c->cfg.width;
-    {  // the canonical rows scattered into the hot rows and cold records
-        int32_t *tmp = nullptr;
-        ST_HIP(hipMalloc(&tmp, pitch * ST_NSTAT));
-        // the padding envs (columns n .. stride) keep their current counters
-        hipError_t e = st::launch_get_stats(params(c), tmp, nullptr);
-        if (e == hipSuccess) e = hipDeviceSynchronize();
-        if (e == hipSuccess) e = hipMemcpy2D(tmp, pitch, in, row, row, ST_NSTAT, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = st::launch_set_stats(params(c), tmp, nullptr);
-        if (e == hipSuccess) e = hipDeviceSynchronize();
-        (void)hipFree(tmp);
-        if (e != hipSuccess) return hip_fail(e, "st_load: counters");
-    }
+    ST_HIP(hipMemcpy2D(c->stats, pitch, in, row, row, ST_NSTAT, hipMemcpyHostToDevice));
     in += row * ST_NSTAT;
     const size_t mrow = (size_t)st::kMtN * 4, mpitch = (size_t)st::kMtPitch * 4;
     ST_HIP(hipMemcpy2D(c->mt, mpitch, in, mrow, mrow, (size_t)c->n, hipMemcpyHostToDevice));

@@ -23,41 +23,9 @@ constexpr int64_t kMtPadBack = 64;
 // st_rollout: per-phase cycle totals of the logic / draw / output wave
 // (words 0-15 / 16-31 / 32-47)
 constexpr int kStampWords = 48;
-constexpr int kPieceRow = ST_STAT_PIECE;     // canonical rows 0..14 (counters + piece)
+constexpr int kPieceRow = ST_STAT_PIECE;     // rows 0..14 (counters + piece) move every step
 constexpr int kHotRows = ST_STAT_PIECE + 1;
-constexpr int kHotQ = (kHotRows * 16 + kWave - 1) / kWave;  // 16-B slots per lane (staged rows 0..15)
-
-// ---- State layout in HBM (round 5: hot rows + per-env cold record) ----
-// Every env reads its board and four HOT words every step; the counters that
-// only a lock touches live in a per-env COLD record that only locking envs
-// read and write.
-//   hot  u32 [kNHot][stride] (SoA):  time | piece word | MT word | draw word
-//   cold i32 [stride][kCold] (AoS, 64 B per env, 64-B aligned):
-//        score lines holes piece_height deaths | ep_time ep_score ep_lines
-//        ep_holes | shape_counts[7]
-// The DRAW WORD is what the piece draw needs before it knows which envs lock:
-// for each shape i the nibble d_i = max(counts) - counts_i (bits 4i..4i+3;
-// _choose_shape's weights are 5 + d_i, tetris_env.py:183-191) and bit 28 set
-// when some d_i > 15 (then the full counts from the cold record are used).
-// Canonical views (st_get_stats / st_set_stats, st_save / st_load) restore
-// the ST_STAT_* rows.
-constexpr int kHotTime = 0, kHotPiece = 1, kHotMt = 2, kHotDraw = 3, kNHot = 4;
-constexpr int kCold = 16;
-constexpr int kCScore = 0, kCLines = 1, kCHoles = 2, kCHeight = 3, kCDeaths = 4, kCEpTime = 5, kCEpScore = 6,
-              kCEpLines = 7, kCEpHoles = 8, kCCount0 = 9;
-constexpr uint32_t kDwEsc = 1u << 28;
-// the hot / cold home of canonical row r (ST_STAT_*): hot row, or -1 and the
-// cold word
-__host__ __device__ constexpr int stat_hot_row(int r) {
-    return r == ST_STAT_TIME ? kHotTime : r == ST_STAT_PIECE ? kHotPiece : r == ST_STAT_MT_INDEX ? kHotMt : -1;
-}
-__host__ __device__ constexpr int stat_cold_word(int r) {
-    return r == ST_STAT_SCORE ? kCScore : r == ST_STAT_LINES ? kCLines : r == ST_STAT_HOLES ? kCHoles
-         : r == ST_STAT_PIECE_HEIGHT ? kCHeight : r == ST_STAT_DEATHS ? kCDeaths
-         : r == ST_STAT_EP_TIME ? kCEpTime : r == ST_STAT_EP_SCORE ? kCEpScore
-         : r == ST_STAT_EP_LINES ? kCEpLines : r == ST_STAT_EP_HOLES ? kCEpHoles
-         : (r >= ST_STAT_COUNT0 && r < ST_STAT_COUNT0 + 7) ? kCCount0 + (r - ST_STAT_COUNT0) : -1;
-}
+constexpr int kHotQ = (kHotRows * 16 + kWave - 1) / kWave;  // 16-B slots per lane
 
 struct KParams {
     int32_t W, H;
@@ -81,9 +49,8 @@ struct KParams {
     int64_t stride;     // padded env count (multiple of 64) = SoA row stride
     // state
     uint32_t *board;    // [W][stride]
-    uint32_t *hot;      // [kNHot][stride]
-    uint32_t *piece;    // [stride] = hot row kHotPiece
-    int32_t *cold;      // [stride][kCold]
+    uint32_t *piece;    // [stride]
+    int32_t *stats;     // [ST_NSTAT][stride]
     uint32_t *mt;       // [stride][kMtPitch]
     // io
     const uint8_t *actions;  // [n]
@@ -116,9 +83,6 @@ hipError_t launch_grayscale(const KParams &p, const uint32_t *obs, int size, int
 hipError_t launch_unwire(int W, int H, int64_t n_global, int shards, int64_t n_cap, const uint32_t *wire,
                          uint32_t *obs, int32_t *reward, uint8_t *done, hipStream_t s);
 hipError_t launch_check_actions(const uint8_t *a, int64_t n, uint32_t *flag, hipStream_t s);
-// canonical counter rows [ST_NSTAT][stride] <-> hot rows + cold records
-hipError_t launch_get_stats(const KParams &p, int32_t *out, hipStream_t s);
-hipError_t launch_set_stats(const KParams &p, const int32_t *in, hipStream_t s);
 hipError_t launch_gen_actions(uint8_t *out, int64_t n, int64_t t, uint64_t seed, int64_t off,
                               hipStream_t s);
 

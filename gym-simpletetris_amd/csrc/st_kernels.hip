@@ -3,12 +3,11 @@
 // Hot path: TetrisEngine.step (/root/reference/gym_simpletetris/envs/tetris_env.py:243-304)
 // for N independent envs, one env per lane, one wave (64 envs) per workgroup.
 //
-// Data layout (HBM; st_internal.h):
+// Data layout (HBM, SoA over envs, row stride = padded env count):
 //   board  u32 [W][stride]  bit y of word (x, e) = board[x, y]  (the reference's
 //          (width, height) array, tetris_env.py:140, one bit-packed u32 per x)
-//   hot    u32 [4][stride]  time | piece word (id | rot<<3 | ax<<5 | ay<<11 |
-//          lock<<17) | MT word | draw word: read by every env every step
-//   cold   i32 [stride][16] per-env record of the counters only a lock touches
+//   piece  u32 [stride]     id | rot<<3 | ax<<5 | ay<<11 | lock<<17
+//   stats  i32 [ST_NSTAT][stride]
 //   mt     u32 [stride][624] per-env CPython MT19937 words (env-contiguous so a
 //          wave can twist one env's state with coalesced 256-B accesses)
 // Every load a step needs is issued up front (coalesced, 4 B/lane); the board
@@ -191,6 +190,24 @@ constexpr int kNT = 2;
 // step: K = 2,000 4.67-4.72 -> 4.64-4.67 us, profiles/r03/ab_step_lprio.txt).
 constexpr int kDrawPrio = 2;
 constexpr int kLogicPrio = 1;
+// A/B knobs (round 5, partial-write study): store whole rows instead of the
+// changed 16-B groups / lanes only (same values, full lines written)
+#ifndef ST_FULL_BOARD
+#define ST_FULL_BOARD 0
+#endif
+#ifndef ST_FULL_LCNT
+#define ST_FULL_LCNT 0
+#endif
+#ifndef ST_FULL_DCNT
+#define ST_FULL_DCNT 0
+#endif
+// A/B knob (round 5): st_step's draw wave stores the spawned shape's count
+// right after B1 (known since the step started: the preview's shape) instead
+// of at the end of its chain (same-step auto-reset; lanes without a preview
+// keep the late store)
+#ifndef ST_EARLY_COUNT
+#define ST_EARLY_COUNT 0
+#endif
 // A/B knob (round 5): st_rollout's draw wave keeps each
 // lane's 16-word MT window in LDS (wb[j][lane]) instead of registers: the
 // words at the lane's offset are read by address (ds_read2st64) instead of
@@ -198,6 +215,12 @@ constexpr int kLogicPrio = 1;
 // 16 register selects
 #ifndef ST_RO_LDSWIN
 #define ST_RO_LDSWIN 0
+#endif
+// A/B knob (round 5): st_step's logic wave stores its lock-path counters, the
+// episode rows of a reset and the clock right after the lock path, before the
+// obs / board store burst, instead of at the end of its chain
+#ifndef ST_EARLY_CNT
+#define ST_EARLY_CNT 0
 #endif
 template <int AUX = 0>
 __device__ __forceinline__ void buf_store16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
@@ -668,48 +691,6 @@ __device__ __forceinline__ DrawPar draw_par(const int32_t (&cnt)[7]) {
     }
     return d;
 }
-// ---- the draw word (hot row kHotDraw; st_internal.h) ----
-// d_i = max(counts) - counts_i in nibble i, kDwEsc when some d_i > 15.
-__device__ __forceinline__ uint32_t dw_from_counts(const int32_t (&c)[7]) {
-    int32_t mx = c[0];
-#pragma unroll
-    for (int i = 1; i < 7; ++i) mx = c[i] > mx ? c[i] : mx;
-    uint32_t w = 0, big = 0;
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-        const uint32_t d = (uint32_t)mx - (uint32_t)c[i];  // exact as unsigned for any int32 counts
-        big |= d > 15u ? 1u : 0u;
-        w |= (d & 15u) << (4 * i);
-    }
-    return big ? (w | kDwEsc) : w;
-}
-// draw_par of the counts the draw word describes after shape s spawns
-// (counts[s] += 1: _new_piece, tetris_env.py:199) -- the preview draw's
-// parameters before anything but the hot words is known.  `ok` false: the
-// word was escaped or a distance would pass 15 (the full counts decide).
-// `wn`: the draw word after the spawn (valid where `ok`).
-__device__ __forceinline__ DrawPar draw_par_dw(uint32_t dw, int s, bool &ok, uint32_t &wn) {
-    const uint32_t sh = 4u * (uint32_t)s;
-    const uint32_t ds = (dw >> sh) & 15u;
-    // s at the maximum: it becomes the sole maximum, every other distance
-    // grows by one (a 15 grows past the nibble: escaped); else d_s shrinks
-    const uint32_t x = (dw & 0xFFFFFFFu) ^ 0xFFFFFFFu;  // nibbles equal to 15 -> 0
-    const bool has15 = ((x - 0x1111111u) & ~x & 0x8888888u) != 0u;
-    ok = !(dw & kDwEsc) && !(ds == 0u && has15);
-    const uint32_t w = ds ? dw - (1u << sh) : (dw & 0xFFFFFFFu) + 0x1111111u - (1u << sh);
-    wn = w;
-    DrawPar d;
-    int32_t sum = 0;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        sum += 5 + (int32_t)((w >> (4 * i)) & 15u);
-        d.th[i] = sum;
-    }
-    d.n = (uint32_t)(sum + 5 + (int32_t)((w >> 24) & 15u));
-    d.kb = 32 - __builtin_clz(d.n);
-    return d;
-}
-
 // The draw itself, for the lanes with `need` (see draw_shape): the window's
 // words are tempered 4 at a time (acceptance >= 1/2, ~0.7 typically; a second
 // group of 4 only in waves where a lane rejected 4 in a row), and the shape is
@@ -1059,96 +1040,6 @@ __device__ __forceinline__ void lds_flag_wait_ge(uint32_t *f, uint32_t v) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// ---- canonical counter rows <-> hot rows + cold records (st_internal.h) ----
-// The kernels that keep every counter of their envs in LDS (st_step_vec,
-// the rollouts) stage the ST_STAT_* rows a role reads into SS[row][lane]
-// (each lane its own env: the cold record is contiguous per env) and store
-// them back at the end.  Logic role: time, piece, score .. deaths; draw role:
-// the shape counts and the MT word.
-struct CanonRows {
-    uint32_t h0, h1;  // logic: time, piece word | draw: MT word
-    uint4 c0, c1;     // logic: cold words 0..7 | draw: cold words 8..15
-};
-template <bool LOGIC>
-__device__ __forceinline__ void canon_load(const KParams &p, int64_t e, CanonRows &r) {
-    const int64_t sd = p.stride;
-    const uint4 *c = reinterpret_cast<const uint4 *>(p.cold + e * kCold);
-    if constexpr (LOGIC) {
-        r.h0 = p.hot[kHotTime * sd + e];
-        r.h1 = p.hot[kHotPiece * sd + e];
-        r.c0 = c[0];
-        r.c1 = c[1];
-    } else {
-        r.h0 = p.hot[kHotMt * sd + e];
-        r.c0 = c[2];
-        r.c1 = c[3];
-    }
-}
-template <bool LOGIC>
-__device__ __forceinline__ void canon_stage(uint32_t *SS, int lane, const CanonRows &r) {
-    auto w = [&](int row, uint32_t v) { SS[row * kWave + lane] = v; };
-    if constexpr (LOGIC) {
-        w(ST_STAT_TIME, r.h0);
-        w(ST_STAT_PIECE, r.h1);
-        w(ST_STAT_SCORE, r.c0.x);
-        w(ST_STAT_LINES, r.c0.y);
-        w(ST_STAT_HOLES, r.c0.z);
-        w(ST_STAT_PIECE_HEIGHT, r.c0.w);
-        w(ST_STAT_DEATHS, r.c1.x);
-    } else {
-        static_assert(kCCount0 == 9, "counts at cold words 9..15");
-        w(ST_STAT_MT_INDEX, r.h0);
-        w(ST_STAT_COUNT0 + 0, r.c0.y);
-        w(ST_STAT_COUNT0 + 1, r.c0.z);
-        w(ST_STAT_COUNT0 + 2, r.c0.w);
-        w(ST_STAT_COUNT0 + 3, r.c1.x);
-        w(ST_STAT_COUNT0 + 4, r.c1.y);
-        w(ST_STAT_COUNT0 + 5, r.c1.z);
-        w(ST_STAT_COUNT0 + 6, r.c1.w);
-    }
-}
-// the staged rows of a role back to HBM (draw role: + the draw word from the
-// counts); buffer stores, `on` false: dropped
-template <bool LOGIC>
-__device__ __forceinline__ void canon_store(const KParams &p, int64_t e, const uint32_t *SS, int lane, bool on) {
-    const uint32_t sd = (uint32_t)p.stride;
-    auto ss = [&](int row) -> uint32_t { return SS[row * kWave + lane]; };
-    const auto rh = buf_rsrc(p.hot, (uint32_t)kNHot * sd * 4u);
-    const auto rc = buf_rsrc(p.cold, sd * (uint32_t)kCold * 4u);
-    const uint32_t eh = (uint32_t)e * 4u, ec = (uint32_t)e * (uint32_t)(kCold * 4);
-    if constexpr (LOGIC) {
-        __builtin_amdgcn_raw_buffer_store_b32(ss(ST_STAT_TIME), rh, on ? eh + (uint32_t)kHotTime * sd * 4u : kOff, 0, kNT);
-        __builtin_amdgcn_raw_buffer_store_b32(ss(ST_STAT_PIECE), rh, on ? eh + (uint32_t)kHotPiece * sd * 4u : kOff, 0, kNT);
-        buf_store16<kNT>(rc, on ? ec : kOff, make_uint4(ss(ST_STAT_SCORE), ss(ST_STAT_LINES), ss(ST_STAT_HOLES),
-                                                       ss(ST_STAT_PIECE_HEIGHT)));
-        __builtin_amdgcn_raw_buffer_store_b32(ss(ST_STAT_DEATHS), rc, on ? ec + (uint32_t)kCDeaths * 4u : kOff, 0, kNT);
-    } else {
-        int32_t c[7];
-#pragma unroll
-        for (int i = 0; i < 7; ++i) c[i] = (int32_t)ss(ST_STAT_COUNT0 + i);
-        __builtin_amdgcn_raw_buffer_store_b32(ss(ST_STAT_MT_INDEX), rh, on ? eh + (uint32_t)kHotMt * sd * 4u : kOff, 0, kNT);
-        __builtin_amdgcn_raw_buffer_store_b32(dw_from_counts(c), rh, on ? eh + (uint32_t)kHotDraw * sd * 4u : kOff, 0, kNT);
-        // counts: cold words 9 | 10..11 | 12..15 (ep_holes, word 8, is not touched)
-        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)c[0], rc, on ? ec + 36u : kOff, 0, kNT);
-        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-        const u32x2 c12 = {(uint32_t)c[1], (uint32_t)c[2]};
-        __builtin_amdgcn_raw_buffer_store_b64(c12, rc, on ? ec + 40u : kOff, 0, kNT);
-        buf_store16<kNT>(rc, on ? ec + 48u : kOff, make_uint4((uint32_t)c[3], (uint32_t)c[4], (uint32_t)c[5], (uint32_t)c[6]));
-    }
-}
-// the finished episode's counters of a same-step reset (ST_AUTORESET_SAME_STEP):
-// cold words 5..8
-__device__ __forceinline__ void store_ep(const KParams &p, int64_t e, int32_t t, int32_t sc, int32_t li, int32_t ho, bool on) {
-    const auto rc = buf_rsrc(p.cold, (uint32_t)p.stride * (uint32_t)kCold * 4u);
-    const uint32_t ec = (uint32_t)e * (uint32_t)(kCold * 4);
-    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)t, rc, on ? ec + (uint32_t)kCEpTime * 4u : kOff, 0, kNT);
-    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)sc, rc, on ? ec + (uint32_t)kCEpScore * 4u : kOff, 0, kNT);
-    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)li, rc, on ? ec + (uint32_t)kCEpLines * 4u : kOff, 0, kNT);
-    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)ho, rc, on ? ec + (uint32_t)kCEpHoles * 4u : kOff, 0, kNT);
-}
-// SS row of st_step's staged draw word (canonical row 15 = ep_time is never staged)
-constexpr int kSsDraw = 15;
-
 // ROLE = kRoleL / kRoleD: the logic or the draw wave of a workgroup.
 // KSTEPS == 1: TetrisEngine.step once (st_step); KSTEPS == 0: p.k consecutive
 // steps (k_rollout2, st_rollout above 4 workgroups per CU) with the board and
@@ -1216,9 +1107,9 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     const uint32_t loff = (uint32_t)(lane >> 4) * (uint32_t)sd + 4u * (uint32_t)(lane & 15);
     constexpr int NBQ = ((WT ? WT : kMaxW) + 3) / 4;  // board 4-row groups
     const uint32_t *bsrc = p.board + e0;
-    // (ablation 1024: every wave's hot rows from the first workgroup's lines
-    // -- their HBM reads gone, timing only)
-    const uint32_t *hsrc = p.hot + ((kAblate & 1024u) ? 0 : e0);
+    // (ablation 1024: every wave's counter groups from the first workgroup's
+    // lines -- the counter rows' HBM reads gone, timing only)
+    const uint32_t *ssrc = reinterpret_cast<const uint32_t *>(p.stats) + ((kAblate & 1024u) ? 0 : e0);
     constexpr bool OVP = KSTEPS == 1;
     // st_step (not st_step_vec, whose info snapshot needs every counter of
     // every env): LATE COUNTERS.  The prologue's load burst carries only what
@@ -1232,13 +1123,21 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     // +6% -- its post-B1 chain, window + counts + draw parameters, became the
     // step's -- and was dropped)
     constexpr bool LCL = KSTEPS == 1 && !VEC;
-    // LCL (round 5, the hot / cold layout): the draw wave stages the four hot
-    // rows (time, piece word, MT word, draw word: one 16-B load per lane) --
-    // the draw parameters come from the draw word, the shape counts are read
-    // per locking lane with its MT window after B1; without LCL (st_step_vec,
-    // the two-wave rollout) each role stages its canonical rows (CanonRows)
-    [[maybe_unused]] uint4 hv = make_uint4(0u, 0u, 0u, 0u);
-    [[maybe_unused]] CanonRows crow;
+    // staged counter groups (rows 4q .. 4q + 3): logic 0-1, draw 2-3; with
+    // late rows only what the other role still reads early
+    // LCL: the draw wave stages exactly the rows it reads, the shape counts
+    // and the MT word (rows COUNT0 .. MT_INDEX: two 4-row groups from row 6,
+    // a group's base row needs no alignment) -- round 4 staged rows 4..15,
+    // 16 B per env more
+    static_assert(ST_STAT_MT_INDEX == ST_STAT_COUNT0 + 7, "counts and MT word: 8 consecutive rows");
+    auto mine_q = [&](int q) {
+        if constexpr (LCL) return ROLE == kRoleD && (q == 1 || q == 2);
+        return (ROLE == kRoleL) == (q < 2);
+    };
+    auto qbase = [&](int q) -> int {  // first stats row of staged group q
+        if constexpr (LCL) return ST_STAT_COUNT0 + 4 * (q - 1);
+        return 4 * q;
+    };
     // Rows past the last real row (board padding, counter row 15) re-read the
     // last row -- the same cache line another lane fetches -- instead of
     // fetching padding; the loads stay unconditional (a load under a branch
@@ -1255,9 +1154,12 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 bv[q] = *reinterpret_cast<const uint4 *>(bsrc + (size_t)(4 * q) * sd +
                                                          (4 * q + 4 <= W ? loff : clamp_off(q, W)));
     }
-    static_assert(kNHot == 4, "the hot rows are one 4-row group");
-    if constexpr (LCL && ROLE == kRoleD) hv = *reinterpret_cast<const uint4 *>(hsrc + loff);
-    if constexpr (!LCL) canon_load<ROLE == kRoleL>(p, e, crow);
+    uint4 sv[kHotQ];
+#pragma unroll
+    for (int q = 0; q < kHotQ; ++q)
+        if (mine_q(q))
+            sv[q] = *reinterpret_cast<const uint4 *>(ssrc + (size_t)qbase(q) * sd +
+                                                     (qbase(q) + 4 <= kHotRows ? loff : clamp_off(q, kHotRows)));
     const int K = KSTEPS ? KSTEPS : p.k;
     // two-wave st_step: the logic wave also builds the next-generation block
     // (the draw wave's chain is the longer one).  (Measured and dropped: the
@@ -1275,8 +1177,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     constexpr bool DL = KSTEPS == 1 && ROLE == kRoleL;
     [[maybe_unused]] uint32_t pw_d = 0, tm_d = 0;
     if constexpr (DL) {
-        pw_d = p.hot[(int64_t)kHotPiece * sd + e];
-        tm_d = p.hot[(int64_t)kHotTime * sd + e];
+        pw_d = p.piece[e];
+        tm_d = reinterpret_cast<const uint32_t *>(p.stats)[(int64_t)ST_STAT_TIME * sd + e];
     }
     // The piece table, lane i = entry i, from immediates (under the load
     // latency; no memory access: a __constant__ load gets sunk by the
@@ -1335,13 +1237,9 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             }
         }
     }
-    if constexpr (LCL && ROLE == kRoleD) {
-        // hot row lrow -> its SS row: time 0, piece 14, MT word 13, draw word 15
-        const int hr = lrow == kHotTime ? ST_STAT_TIME : lrow == kHotPiece ? ST_STAT_PIECE
-                       : lrow == kHotMt ? ST_STAT_MT_INDEX : kSsDraw;
-        *reinterpret_cast<uint4 *>(&SS[hr * kWave + lcc]) = hv;
-    }
-    if constexpr (!LCL) canon_stage<ROLE == kRoleL>(SS, lane, crow);
+#pragma unroll
+    for (int q = 0; q < kHotQ; ++q)
+        if (mine_q(q)) *reinterpret_cast<uint4 *>(&SS[(qbase(q) + lrow) * kWave + lcc]) = sv[q];
     if constexpr (OVP && DO_L) {
 #pragma unroll
         for (int q = 0; q < NBQ; ++q)
@@ -1432,27 +1330,16 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     ST_STAMP(2);
     // LC: the logic wave's lock-path counters, per locking lane (an
     // out-of-range offset elsewhere: no traffic, 0)
-    [[maybe_unused]] uint32_t lcv[8] = {};
+    [[maybe_unused]] uint32_t lcv[5] = {};
     if constexpr (LCL && DO_L) {
-        // the cold record's first 20 B (score, lines, holes, piece_height,
-        // deaths: one 32-B sector of the env's 64-B record)
-        const auto rc = buf_rsrc(p.cold, (uint32_t)sd * (uint32_t)kCold * 4u);
-        // (ablation 8192: from the first workgroup's records -- their HBM reads gone, timing only)
-        const uint32_t eo = ((kAblate & 8192u) ? (uint32_t)lane : (uint32_t)e) * (uint32_t)(kCold * 4);
-        const u32x4 l4 = __builtin_amdgcn_raw_buffer_load_b128(rc, locknow ? eo : kOff, 0, 0);
-        lcv[0] = l4.x;
-        lcv[1] = l4.y;
-        lcv[2] = l4.z;
-        lcv[3] = l4.w;
-#if ST_COLD_FULL
-        const u32x4 l4b = __builtin_amdgcn_raw_buffer_load_b128(rc, locknow ? eo + 16u : kOff, 0, 0);
-        lcv[4] = l4b.x;
-        lcv[5] = l4b.y;
-        lcv[6] = l4b.z;
-        lcv[7] = l4b.w;
-#else
-        lcv[4] = __builtin_amdgcn_raw_buffer_load_b32(rc, locknow ? eo + (uint32_t)kCDeaths * 4u : kOff, 0, 0);
-#endif
+        const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
+        // (ablation 8192: from the first workgroup's lines -- their HBM reads gone, timing only)
+        const uint32_t eo = (kAblate & 8192u) ? (uint32_t)lane * 4u : (uint32_t)e * 4u;
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+            lcv[j] = __builtin_amdgcn_raw_buffer_load_b32(
+                rs, (ST_FULL_LCNT ? real : locknow) ? eo + (uint32_t)(ST_STAT_SCORE + j) * (uint32_t)sd * 4u : kOff,
+                0, 0);
     }
     // the draw wave's next-generation chunk of this step: operands issued
     // before B1, so they arrive while it waits for the lock decision
@@ -1465,25 +1352,16 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     [[maybe_unused]] int32_t cnt[7];
     [[maybe_unused]] DrawPar dpar;
     [[maybe_unused]] int32_t csid = 0;  // the spawned shape's count after the spawn
-    [[maybe_unused]] bool dw_ok = true;   // LCL: dpar from the draw word is valid
-    [[maybe_unused]] uint32_t dwn = 0;    // LCL: the draw word after the spawn
     if constexpr (DO_D) {
         mrs = mt_res(p.mt + e0 * kMtPitch, lane);
         mt_chunk_issue(mrs, mt0, real && !(kAblate & 2u), lane, chunk);
         const int s0 = pv_id(mt0);
-        if constexpr (LCL) {
-            // from the draw word (the counts are read only on the rare
-            // paths): the counts after the preview spawns; dw_ok false (an
-            // escaped word, p ~ 1e-5 per draw): recomputed from the counts
-            dpar = draw_par_dw(ss(kSsDraw), s0, dw_ok, dwn);
-        } else {
 #pragma unroll
-            for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)ss(ST_STAT_COUNT0 + i) + (i == s0);  // _new_piece :199
-            csid = cnt[0];
+        for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)ss(ST_STAT_COUNT0 + i) + (i == s0);  // _new_piece :199
+        csid = cnt[0];
 #pragma unroll
-            for (int i = 1; i < 7; ++i) csid = s0 == i ? cnt[i] : csid;
-            dpar = draw_par(cnt);
-        }
+        for (int i = 1; i < 7; ++i) csid = s0 == i ? cnt[i] : csid;
+        dpar = draw_par(cnt);
     }
     if constexpr (DO_L) {
         const uint64_t m = __ballot(locknow);
@@ -1512,13 +1390,16 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     constexpr int kWin = STEP2 ? 8 : 16;
     MtPre pre;
     if constexpr (DO_D) mt_pre_load<kWin>(mrs, mtst, want_pre, pre);
-    // LCL: the preview shape's count (one cold word per locking lane, issued
-    // with the window, consumed only at the commit): its count after the spawn
-    [[maybe_unused]] uint32_t cs0 = 0;
-    if constexpr (LCL && DO_D) {
-        const auto rc = buf_rsrc(p.cold, (uint32_t)sd * (uint32_t)kCold * 4u);
-        const uint32_t co = (uint32_t)e * (uint32_t)(kCold * 4) + (uint32_t)(kCCount0 + pv_id(mt0)) * 4u;
-        cs0 = __builtin_amdgcn_raw_buffer_load_b32(rc, want_pre ? co : kOff, 0, 0);
+    // ST_EARLY_COUNT: the spawned shape's count, stored now (after the window
+    // loads are issued) where the spawn takes the preview
+    [[maybe_unused]] const bool early_c = ST_EARLY_COUNT && DO_D && STEP2 && !VEC &&
+                                          p.autoreset == ST_AUTORESET_SAME_STEP;
+    if constexpr (ST_EARLY_COUNT && DO_D && STEP2 && !VEC) {
+        const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
+        __builtin_amdgcn_raw_buffer_store_b32(
+            (uint32_t)csid, rs,
+            early_c && locknow && pv_ok(mt0) ? (uint32_t)e * 4u + (uint32_t)(ST_STAT_COUNT0 + pv_id(mt0)) * (uint32_t)sd * 4u
+                                             : kOff, 0, kNT);
     }
 
     // ---------------- logic: lock path (tetris_env.py:263-299) ----------------
@@ -1681,6 +1562,40 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         __builtin_amdgcn_raw_buffer_store_b32(rew, rr, real ? (uint32_t)e * 4u : kOff, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b8((char)(died ? 1 : 0), rd, real ? (uint32_t)e : kOff, 0, 0);
     }
+    // ECNT: the counters known after the lock path stored now (see ST_EARLY_CNT)
+    constexpr bool ECNT = ST_EARLY_CNT && DO_L && STEP2 && LCL && !VEC;
+    if constexpr (ECNT) {
+        if (locknow) {
+            o_score = (int32_t)lcv[0];
+            o_lines = (int32_t)lcv[1];
+            o_holes = (int32_t)lcv[2];
+            o_height = (int32_t)lcv[3];
+            o_deaths = (int32_t)lcv[4];
+            score += o_score;
+            lines += o_lines;
+            deaths += o_deaths;
+            if (!hset) height = o_height;
+        }
+        const auto rs = buf_rsrc(p.stats, (uint32_t)ST_NSTAT * (uint32_t)sd * 4u);
+        const uint32_t eo = (uint32_t)e * 4u;
+        auto put = [&](int r, int32_t v, bool on) {
+            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, on ? eo + (uint32_t)r * (uint32_t)sd * 4u : kOff,
+                                                  0, kNT);
+        };
+        // the finished episode's counters (ST_AUTORESET_SAME_STEP)
+        put(ST_STAT_EP_TIME, time, reset_now);
+        put(ST_STAT_EP_SCORE, score, reset_now);
+        put(ST_STAT_EP_LINES, lines, reset_now);
+        put(ST_STAT_EP_HOLES, holes, reset_now);
+        if (reset_now) time = score = lines = holes = height = 0;
+        const bool cst = !(kAblate & (2048u | 16384u));
+        put(ST_STAT_TIME, time, true);
+        put(ST_STAT_SCORE, score, cst && locknow && score != o_score);
+        put(ST_STAT_LINES, lines, cst && locknow && lines != o_lines);
+        put(ST_STAT_HOLES, holes, cst && locknow && holes != o_holes);
+        put(ST_STAT_PIECE_HEIGHT, height, cst && locknow && height != o_height);
+        put(ST_STAT_DEATHS, deaths, cst && locknow && deaths != o_deaths);
+    }
     if constexpr (DO_L && KSTEPS == 1) {
         // The post-step board never depends on the spawned piece either (a
         // spawn only overlays row 0, which is empty after a non-fatal lock,
@@ -1773,7 +1688,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 v.z &= km.z;
                 v.w &= km.w;
                 // row 4q + lrow; padding rows (>= W) are never dirty
-                const bool dirty = ((bdl >> (4 * q)) & 1u) && 4 * q + lrow < W && !(kAblate & 4096u);
+                const bool dirty = (ST_FULL_BOARD || ((bdl >> (4 * q)) & 1u)) && 4 * q + lrow < W && !(kAblate & 4096u);
                 buf_store16<kNT>(rb, dirty ? boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff, v);
             }
         }
@@ -1797,41 +1712,12 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         uint32_t mt_new = mtst;
         if (!(kAblate & 2u)) {
             mt_win_consume<kWin>(pre);
-            // LCL: all counts (cold words 9..15) only for the rare lanes --
-            // an escaped draw word, or no preview -- whose draws they
-            // decide; the common spawn needs only its shape's count (cs0)
-            [[maybe_unused]] int32_t cf[7] = {};
             const bool need1 = dr_spec && !pv_ok(mt0);
-            if constexpr (LCL) {
-                const bool rare = dr_spec && (!dw_ok || need1);
-                if (__ballot(rare)) {
-                    const auto rc = buf_rsrc(p.cold, (uint32_t)sd * (uint32_t)kCold * 4u);
-                    const uint32_t co = (uint32_t)e * (uint32_t)(kCold * 4) + 32u;
-                    const u32x4 cc0 = __builtin_amdgcn_raw_buffer_load_b128(rc, rare ? co : kOff, 0, 0);
-                    const u32x4 cc1 = __builtin_amdgcn_raw_buffer_load_b128(rc, rare ? co + 16u : kOff, 0, 0);
-                    cf[0] = (int32_t)cc0.y;
-                    cf[1] = (int32_t)cc0.z;
-                    cf[2] = (int32_t)cc0.w;
-                    cf[3] = (int32_t)cc1.x;
-                    cf[4] = (int32_t)cc1.y;
-                    cf[5] = (int32_t)cc1.z;
-                    cf[6] = (int32_t)cc1.w;
-                    const int s0 = pv_id(mt0);
-#pragma unroll
-                    for (int i = 0; i < 7; ++i) cnt[i] = cf[i] + (i == s0);  // _new_piece :199
-                    const DrawPar d2 = draw_par(cnt);
-                    const uint32_t w2 = dw_from_counts(cnt);
-                    if (!dw_ok) {  // an escaped draw word: the counts decide
-                        dpar = d2;
-                        dwn = w2;
-                    }
-                }
-            }
             if (__ballot(need1)) {  // rare: after st_seed / st_mt_sync / a host-written state
                 // the piece first, with the counts before the spawn
                 int32_t c0[7];
 #pragma unroll
-                for (int i = 0; i < 7; ++i) c0[i] = LCL ? cf[i] : (int32_t)ss(ST_STAT_COUNT0 + i);
+                for (int i = 0; i < 7; ++i) c0[i] = (int32_t)ss(ST_STAT_COUNT0 + i);
                 const int pk = draw_shape<kWin, false>(need1, c0, mtst, p.mt + e0 * kMtPitch, sm.S, lane, pre, false);
                 if (need1) {
                     sid = pk;
@@ -1840,16 +1726,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
 #pragma unroll
                     for (int i = 0; i < 7; ++i) csid = pk == i ? cnt[i] : csid;
                 }
-                const DrawPar d1 = draw_par(cnt);
-                if constexpr (LCL) {
-                    const uint32_t w1 = dw_from_counts(cnt);
-                    if (need1) {
-                        dpar = d1;
-                        dwn = w1;
-                    }
-                } else {
-                    dpar = d1;
-                }
+                dpar = draw_par(cnt);
             }
             sm.pick1[lane] = (uint32_t)sid;
             if (lane == 0) lds_flag_set(&sm.f2, (uint32_t)t + 1u);
@@ -1892,23 +1769,25 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             // registers, one coalesced dword per lane and row (no staging
             // through LDS at the end of the chain): the MT word, and the
             // count of the spawned shape (csid, counted above)
-            // (the MT word and the draw word: hot rows; the count: the
-            // spawned shape's cold word; all branch-free buffer stores)
-            const auto rh = buf_rsrc(p.hot, (uint32_t)kNHot * (uint32_t)sd * 4u);
-            const auto rc = buf_rsrc(p.cold, (uint32_t)sd * (uint32_t)kCold * 4u);
-            const uint32_t eo = (uint32_t)e * 4u, ec = (uint32_t)e * (uint32_t)(kCold * 4);
-            // (ablation 2048 / 32768: the lock-path counter stores dropped, timing only)
+            const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
+            const uint32_t eo = (uint32_t)e * 4u;
+            // (ablation 2048: the lock-path counter stores dropped, timing only)
             const bool cst = !(kAblate & (2048u | 32768u));
+            if constexpr (ST_FULL_DCNT && !VEC) {  // (A/B: every lane stores the count rows and the MT word)
+                __builtin_amdgcn_raw_buffer_store_b32(
+                    mt_out, rs, cst && real ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff, 0, kNT);
+#pragma unroll
+                for (int i = 0; i < 7; ++i)
+                    __builtin_amdgcn_raw_buffer_store_b32(
+                        dr && i == sid ? (uint32_t)csid : ss(ST_STAT_COUNT0 + i), rs,
+                        cst && real ? eo + (uint32_t)(ST_STAT_COUNT0 + i) * (uint32_t)sd * 4u : kOff, 0, kNT);
+            } else {
             __builtin_amdgcn_raw_buffer_store_b32(
-                mt_out, rh, cst && !(kAblate & 131072u) && (dr || chunk_me) ? eo + (uint32_t)kHotMt * (uint32_t)sd * 4u : kOff,
-                0, kNT);
-            __builtin_amdgcn_raw_buffer_store_b32(LCL ? dwn : dw_from_counts(cnt), rh,
-                                                  cst && dr ? eo + (uint32_t)kHotDraw * (uint32_t)sd * 4u : kOff, 0, kNT);
-            // (LCL: shape_counts[name] += 1, :199, from the preview's count
-            // word; a lane that drew its piece first counted it above)
-            if constexpr (LCL) csid = pv_ok(mt0) ? (int32_t)cs0 + 1 : csid;
+                mt_out, rs, cst && !(kAblate & 131072u) && (dr || chunk_me) ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff, 0, kNT);
             __builtin_amdgcn_raw_buffer_store_b32(
-                (uint32_t)csid, rc, cst && !(kAblate & 65536u) && dr ? ec + (uint32_t)(kCCount0 + sid) * 4u : kOff, 0, kNT);
+                (uint32_t)csid, rs, cst && !(kAblate & 65536u) && dr && !(early_c && pv_ok(mt0))
+                                        ? eo + (uint32_t)(ST_STAT_COUNT0 + sid) * (uint32_t)sd * 4u : kOff, 0, kNT);
+            }
             if constexpr (VEC) {  // st_step_vec's info snapshot: the shape counts after the step
                 const auto ri = buf_rsrc(p.info, (uint32_t)ST_NSTAT * (uint32_t)p.n * 4u);
 #pragma unroll
@@ -1943,10 +1822,10 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         }
 
         // ---- counters back to the staged rows (tetris_env.py:253, :264-299) ----
-        if constexpr (LCL) {
+        if constexpr (LCL && !ECNT) {
             // the late-loaded counters (issued before B1; the lock path kept
             // deltas) -- absolute values and the old ones for the dirty tests
-            if (locknow) {
+            if (ST_FULL_LCNT || locknow) {
                 o_score = (int32_t)lcv[0];
                 o_lines = (int32_t)lcv[1];
                 o_holes = (int32_t)lcv[2];
@@ -1967,73 +1846,35 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 ep_h = holes;
             }
         }
-        // the finished episode's counters (ST_AUTORESET_SAME_STEP): cold words
-        // 5..8 (st_step: with the deaths word below, two stores)
-        [[maybe_unused]] const int32_t x_t = time, x_s = score, x_l = lines, x_h = holes;
-        if constexpr (!LCL) store_ep(p, e, time, score, lines, holes, reset_now);
-        if (reset_now) time = score = lines = holes = height = 0;
+        if (!ECNT && reset_now) {  // the finished episode's counters (ST_AUTORESET_SAME_STEP)
+            int32_t *st = p.stats + e;
+            st[ST_STAT_EP_TIME * sd] = time;
+            st[ST_STAT_EP_SCORE * sd] = score;
+            st[ST_STAT_EP_LINES * sd] = lines;
+            st[ST_STAT_EP_HOLES * sd] = holes;
+            time = score = lines = holes = height = 0;
+        }
         // st_step stores only the counter rows that changed (per env)
         if constexpr (STEP2) {
             // st_step: straight from the registers, one coalesced dword per
             // lane and changed row (no staging through LDS at the end of the
             // chain), unconditional stores with an out-of-range offset
             // where a row did not change
-            // the clock and the piece word: hot rows; the lock-path counters:
-            // the cold record's words 0..4
-            const auto rh = buf_rsrc(p.hot, (uint32_t)kNHot * (uint32_t)sd * 4u);
-            const auto rc = buf_rsrc(p.cold, (uint32_t)sd * (uint32_t)kCold * 4u);
-            const uint32_t eo = (uint32_t)e * 4u, ec = (uint32_t)e * (uint32_t)(kCold * 4);
-            auto put = [&](int r, int32_t v, bool on) {  // r: a compile-time ST_STAT_* row
-                const int hr = stat_hot_row(r), cw = stat_cold_word(r);
-                if (hr >= 0)
-                    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rh, on ? eo + (uint32_t)hr * (uint32_t)sd * 4u : kOff,
-                                                          0, kNT);
-                else
-                    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rc, on ? ec + (uint32_t)cw * 4u : kOff, 0, kNT);
+            const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
+            const uint32_t eo = (uint32_t)e * 4u;
+            auto put = [&](int r, int32_t v, bool on) {
+                __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, on ? eo + (uint32_t)r * (uint32_t)sd * 4u : kOff,
+                                                      0, kNT);
             };
-            put(ST_STAT_TIME, time, true);
+            if constexpr (!ECNT) put(ST_STAT_TIME, time, true);
             put(kPieceRow, (int32_t)pw_out, true);
-            const bool cst = !(kAblate & (2048u | 16384u));  // (ablation: lock-path counter stores dropped)
-            if constexpr (LCL) {
-                // the cold record's words 0..8 in at most three stores per
-                // lane (one 64-B record: a store per word would cost the
-                // memory pipeline a record's segment per instruction):
-                // words 0..3 where one of them changed; a same-step reset's
-                // words 4..7 (deaths, ep_time, ep_score, ep_lines) and 8
-                // (ep_holes); else the deaths word where a death counted
-                const bool c4 = locknow && (score != o_score || lines != o_lines || holes != o_holes || height != o_height);
-                u32x4 v4 = {(uint32_t)score, (uint32_t)lines, (uint32_t)holes, (uint32_t)height};
-#if ST_COLD_FULL
-                // (variant: whole 32-B sectors -- words 0..7 rewritten as loaded
-                // where anything in them changed)
-                const bool c8 = c4 || (locknow && deaths != o_deaths);
-                u32x4 w4 = {(uint32_t)deaths, reset_now ? (uint32_t)x_t : lcv[5], reset_now ? (uint32_t)x_s : lcv[6],
-                            reset_now ? (uint32_t)x_l : lcv[7]};
-                __builtin_amdgcn_raw_buffer_store_b128(v4, rc, cst && c8 ? ec : kOff, 0, kNT);
-                __builtin_amdgcn_raw_buffer_store_b128(w4, rc, cst && c8 ? ec + 16u : kOff, 0, kNT);
-                __builtin_amdgcn_raw_buffer_store_b32((uint32_t)x_h, rc, reset_now ? ec + (uint32_t)kCEpHoles * 4u : kOff, 0,
-                                                      kNT);
-                if constexpr (false)
-#endif
-                {
-                __builtin_amdgcn_raw_buffer_store_b128(v4, rc, cst && c4 ? ec : kOff, 0, kNT);
-                if (__ballot(reset_now)) {
-                    u32x4 e4 = {(uint32_t)deaths, (uint32_t)x_t, (uint32_t)x_s, (uint32_t)x_l};
-                    __builtin_amdgcn_raw_buffer_store_b128(e4, rc, reset_now ? ec + (uint32_t)kCDeaths * 4u : kOff, 0, kNT);
-                    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)x_h, rc, reset_now ? ec + (uint32_t)kCEpHoles * 4u : kOff,
-                                                          0, kNT);
-                }
-                __builtin_amdgcn_raw_buffer_store_b32(
-                    (uint32_t)deaths, rc, cst && !reset_now && locknow && deaths != o_deaths ? ec + (uint32_t)kCDeaths * 4u : kOff,
-                    0, kNT);
-                }
-            } else {
-                put(ST_STAT_SCORE, score, cst && locknow && score != o_score);
-                put(ST_STAT_LINES, lines, cst && locknow && lines != o_lines);
-                put(ST_STAT_HOLES, holes, cst && locknow && holes != o_holes);
-                put(ST_STAT_PIECE_HEIGHT, height, cst && locknow && height != o_height);
-                put(ST_STAT_DEATHS, deaths, cst && locknow && deaths != o_deaths);
-            }
+            const bool cst = !ECNT && !(kAblate & (2048u | 16384u));  // (ablation: lock-path counter stores dropped)
+            const bool fl = ST_FULL_LCNT && LCL && real;  // (A/B: every lane stores every row)
+            put(ST_STAT_SCORE, score, cst && (fl || (locknow && score != o_score)));
+            put(ST_STAT_LINES, lines, cst && (fl || (locknow && lines != o_lines)));
+            put(ST_STAT_HOLES, holes, cst && (fl || (locknow && holes != o_holes)));
+            put(ST_STAT_PIECE_HEIGHT, height, cst && (fl || (locknow && height != o_height)));
+            put(ST_STAT_DEATHS, deaths, cst && (fl || (locknow && deaths != o_deaths)));
             if constexpr (VEC) {
                 // st_step_vec's info snapshot: this wave's rows for every env
                 // (locking lanes from the registers, the others unchanged)
@@ -2235,10 +2076,21 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         }
     }
     // rollout: the staged counter rows, each wave the rows it owns (logic:
-    // time, score .. deaths, the piece word; draw: the shape counts, the MT
-    // word, and the draw word from the counts); st_step stored its changed
-    // rows per lane above
-    if constexpr (!STEP2) canon_store<ROLE == kRoleL>(p, e, SS, lane, true);
+    // 0-5 and the piece row, draw: the shape counts and the MT word); st_step
+    // stored its changed rows per lane above
+    constexpr uint32_t kRowsD = ((1u << 7) - 1u) << ST_STAT_COUNT0 | 1u << ST_STAT_MT_INDEX;
+    constexpr uint32_t kOwn = ROLE == kRoleD ? kRowsD : ((1u << kHotRows) - 1u) & ~kRowsD;
+    const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
+    const uint32_t soff = (uint32_t)e0 * 4u + loff * 4u;
+#pragma unroll
+    for (int q = 0; q < kHotQ; ++q) {
+        if constexpr (STEP2) break;
+        // row 15 (ep_time) is never staged: it is stored per lane on a reset
+        if (((kOwn >> (4 * q)) & 0xFu) == 0u) continue;
+        const bool st = (kOwn >> (4 * q + lrow)) & 1u;
+        buf_store16<kNT>(rs, st ? soff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff,
+                         *reinterpret_cast<const uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]));
+    }
     if constexpr (STAMP && KSTEPS != 1) {
         // rollout stamp build: words [0, 16) of the workgroup's slot the
         // logic wave's per-phase cycle totals (stamp index i), [16, 32) the
@@ -2419,20 +2271,21 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
     auto tab = [&](int i) -> uint2 { return *reinterpret_cast<const uint2 *>(&sm.T2[2 * i]); };
     auto col = [&](uint32_t *P, int x) -> uint32_t & { return P[(x + kPad) * kWave + lane]; };
 
-    // ---- prologue: state into LDS (board: 16 B per lane, transposed), B0 ----
-    // logic: board + its canonical counter rows (time, score .. deaths,
-    // piece); draw: the shape counts and the MT word, the walls, the piece
-    // table; output: the zeroed overlay plane
+    // ---- prologue: state into LDS (16 B per lane, transposed), B0 ----
+    // logic: board + counter groups 0-1 (time .. count1); draw: counter
+    // groups 2-3 (count2 .. MT word, piece), the walls, the piece table;
+    // output: the zeroed overlay plane
     const uint32_t *bsrc = p.board + e0;
+    const uint32_t *ssrc = reinterpret_cast<const uint32_t *>(p.stats) + e0;
     if constexpr (ROLE == kRoleL) {
-        uint4 bv[NBQ];
-        CanonRows crow;
+        uint4 bv[NBQ], sv[2];
 #pragma unroll
         for (int q = 0; q < NBQ; ++q)
             if (WT || 4 * q < W)
                 bv[q] = *reinterpret_cast<const uint4 *>(bsrc + (size_t)(4 * q) * sd +
                                                          (4 * q + 4 <= W ? loff : clamp_off(q, W)));
-        canon_load<true>(p, e, crow);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) sv[q] = *reinterpret_cast<const uint4 *>(ssrc + (size_t)(4 * q) * sd + loff);
 #pragma unroll
         for (int q = 0; q < NBQ; ++q) {
             if (WT || 4 * q < W) {
@@ -2446,11 +2299,15 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 if (4 * q + lrow < W) *reinterpret_cast<uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]) = v;
             }
         }
-        canon_stage<true>(SS, lane, crow);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) *reinterpret_cast<uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]) = sv[q];
         if (lane == 0) sm.fo = 0u;
     } else if constexpr (ROLE == kRoleD) {
-        CanonRows crow;
-        canon_load<false>(p, e, crow);
+        uint4 sv[2];
+#pragma unroll
+        for (int q = 2; q < kHotQ; ++q)
+            sv[q - 2] = *reinterpret_cast<const uint4 *>(ssrc + (size_t)(4 * q) * sd +
+                                                         (4 * q + 4 <= kHotRows ? loff : clamp_off(q, kHotRows)));
         uint32_t tab_m = 0, tab_g = 0;
 #pragma unroll
         for (int i = 0; i < 28; ++i) {
@@ -2474,7 +2331,8 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 sm.F4[4 * lane + 3] = (float)((lane >> 3) & 1);
             }
         }
-        canon_stage<false>(SS, lane, crow);
+#pragma unroll
+        for (int q = 2; q < kHotQ; ++q) *reinterpret_cast<uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]) = sv[q - 2];
         if (lane == 0) {
             sm.fl = 0u;
             sm.fd = 0u;
@@ -3218,8 +3076,13 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                         __builtin_amdgcn_raw_buffer_store_b32(sm.rw[t & 1][lane], rr, real ? (uint32_t)e * 4u : kOff, 0, 0);
                         __builtin_amdgcn_raw_buffer_store_b8((char)dn, rd, real ? (uint32_t)e : kOff, 0, 0);
                         const bool rs_now = dn != 0u && p.autoreset == ST_AUTORESET_SAME_STEP;
-                        store_ep(p, e, (int32_t)sm.ep[t & 1][0][lane], (int32_t)sm.ep[t & 1][1][lane],
-                                 (int32_t)sm.ep[t & 1][2][lane], (int32_t)sm.ep[t & 1][3][lane], rs_now);
+                        const auto rs = buf_rsrc(p.stats, (uint32_t)ST_NSTAT * (uint32_t)sd * 4u);
+                        const uint32_t eo = (uint32_t)e * 4u;
+                        constexpr int kEpRow[4] = {ST_STAT_EP_TIME, ST_STAT_EP_SCORE, ST_STAT_EP_LINES, ST_STAT_EP_HOLES};
+#pragma unroll
+                        for (int k = 0; k < 4; ++k)
+                            __builtin_amdgcn_raw_buffer_store_b32(sm.ep[t & 1][k][lane], rs,
+                                                                  rs_now ? eo + (uint32_t)kEpRow[k] * (uint32_t)sd * 4u : kOff, 0, 0);
                     }
                 }
                 if constexpr (!EARLY)
@@ -3237,9 +3100,21 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
         if constexpr (CHO) chunk_done();
         wg_barrier();
     }
-    // ---- counter rows this wave owns (logic: time, score .. deaths, the
-    // piece word; draw: the shape counts, the MT word, the draw word) ----
-    if constexpr (ROLE != kRoleO) canon_store<ROLE == kRoleL>(p, e, SS, lane, true);
+    // ---- counter rows this wave owns (logic: 0-5 and the piece row, draw:
+    // the shape counts and the MT word) ----
+    if constexpr (ROLE != kRoleO) {
+        constexpr uint32_t kRowsD = ((1u << 7) - 1u) << ST_STAT_COUNT0 | 1u << ST_STAT_MT_INDEX;
+        constexpr uint32_t kOwn = ROLE == kRoleD ? kRowsD : ((1u << kHotRows) - 1u) & ~kRowsD;
+        const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
+        const uint32_t soff = (uint32_t)e0 * 4u + loff * 4u;
+#pragma unroll
+        for (int q = 0; q < kHotQ; ++q) {
+            if (((kOwn >> (4 * q)) & 0xFu) == 0u) continue;
+            const bool st = (kOwn >> (4 * q + lrow)) & 1u;
+            buf_store16<kNT>(rs, st ? soff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff,
+                             *reinterpret_cast<const uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]));
+        }
+    }
     if constexpr (STAMP) {
         uint64_t *slot = p.stamps + (int64_t)blockIdx.x * kStampWords + 16 * (ROLE == kRoleL ? 0 : ROLE == kRoleD ? 1 : 2);
         if (lane == 0) {
@@ -3288,11 +3163,11 @@ __global__ __launch_bounds__(kWave) void k_reset(KParams p) {
     const int64_t e = e0 + lane;
     const int64_t sd = p.stride;
     const bool m = e < p.n && (p.mask == nullptr || p.mask[e] != 0);
-    int32_t *cr = p.cold + e * kCold;  // the env's cold record
+    int32_t *st = p.stats + e;
     int32_t cnt[7];
 #pragma unroll
-    for (int i = 0; i < 7; ++i) cnt[i] = cr[kCCount0 + i];
-    uint32_t mtst = p.hot[kHotMt * sd + e];
+    for (int i = 0; i < 7; ++i) cnt[i] = st[(ST_STAT_COUNT0 + i) * sd];
+    uint32_t mtst = (uint32_t)st[ST_STAT_MT_INDEX * sd];
     const uint32_t mt0 = mtst;
     const uint32_t pw = p.piece[e];
     const MtPre nopre{};
@@ -3308,15 +3183,14 @@ __global__ __launch_bounds__(kWave) void k_reset(KParams p) {
     const uint32_t m1 = mtst;
     const int npv = draw_shape<8, false>(m, cnt, mtst, p.mt + e0 * kMtPitch, S, lane, nopre, false);
     if (m) {
-        p.hot[kHotTime * sd + e] = 0;
-        cr[kCScore] = 0;
-        cr[kCHoles] = 0;
-        cr[kCLines] = 0;
-        cr[kCHeight] = 0;
-        p.hot[kHotMt * sd + e] = pv_pack(mtst, npv, mt_consumed(m1, mtst));
+        st[ST_STAT_TIME * sd] = 0;
+        st[ST_STAT_SCORE * sd] = 0;
+        st[ST_STAT_HOLES * sd] = 0;
+        st[ST_STAT_LINES * sd] = 0;
+        st[ST_STAT_PIECE_HEIGHT * sd] = 0;
+        st[ST_STAT_MT_INDEX * sd] = (int32_t)pv_pack(mtst, npv, mt_consumed(m1, mtst));
 #pragma unroll
-        for (int i = 0; i < 7; ++i) cr[kCCount0 + i] = cnt[i];
-        p.hot[kHotDraw * sd + e] = dw_from_counts(cnt);
+        for (int i = 0; i < 7; ++i) st[(ST_STAT_COUNT0 + i) * sd] = cnt[i];
         for (int x = 0; x < p.W; ++x) p.board[x * sd + e] = 0u;
         p.piece[e] = pack_piece(sid, 0, p.W / 2, 0, (int)(pw >> 17));
     }
@@ -3376,12 +3250,11 @@ __global__ void k_seed(KParams p) {
     nx[kMtN - 1] = nx[396] ^ mt_mix(g[kMtN - 1], nx[0]);
 
     const int64_t sd = p.stride;
-    int32_t *cr = p.cold + e * kCold;
-    for (int w = 0; w < kCold; ++w) cr[w] = 0;
-    cr[kCScore] = -1;                   // :166
-    p.hot[kHotTime * sd + e] = ~0u;     // time = -1, :165
-    p.hot[kHotMt * sd + e] = mt_pack(kMtN, kMtN, 0);  // index 624, next generation complete
-    p.hot[kHotDraw * sd + e] = 0u;      // all counts 0
+    int32_t *st = p.stats + e;
+    for (int r = 0; r < ST_NSTAT; ++r) st[r * sd] = 0;
+    st[ST_STAT_TIME * sd] = -1;   // :165
+    st[ST_STAT_SCORE * sd] = -1;  // :166
+    st[ST_STAT_MT_INDEX * sd] = (int32_t)mt_pack(kMtN, kMtN, 0);  // index 624, next generation complete
     for (int x = 0; x < p.W; ++x) p.board[x * sd + e] = 0u;
     p.piece[e] = pack_piece(0, 0, p.W / 2, 0, 0);
 }
@@ -3400,8 +3273,8 @@ __global__ __launch_bounds__(kWave) void k_mt_sync(KParams p) {
     const int lane = threadIdx.x;
     const int64_t e0 = (int64_t)blockIdx.x * kWave;
     const int64_t e = e0 + lane;
-    uint32_t *row = p.hot + (int64_t)kHotMt * p.stride;
-    const uint32_t r = row[e];
+    int32_t *row = p.stats + (int64_t)ST_STAT_MT_INDEX * p.stride;
+    const uint32_t r = (uint32_t)row[e];
     int idx = (int)(r & 0x3FFu);
     uint32_t cur = (r >> 20) & 1u;
     if (pv_ok(r)) {
@@ -3436,7 +3309,7 @@ __global__ __launch_bounds__(kWave) void k_mt_sync(KParams p) {
             if (i < kMtN) g[i] = t[q];
         }
     }
-    if (r != (uint32_t)idx) row[e] = (uint32_t)idx;
+    if (r != (uint32_t)idx) row[e] = idx;
 }
 
 // ---------------------------------------------------------------- render
@@ -3474,7 +3347,7 @@ __global__ __launch_bounds__(256) void k_export(KParams p, int64_t env, const ui
                                                uint32_t *out) {
     const int W = p.W, H = p.H;
     const int head = W + 2 + ST_NSTAT;
-    const uint32_t r = p.hot[(int64_t)kHotMt * p.stride + env];
+    const uint32_t r = (uint32_t)p.stats[(int64_t)ST_STAT_MT_INDEX * p.stride + env];
     int idx = (int)(r & 0x3FFu);
     uint32_t cur = (r >> 20) & 1u;
     if (pv_ok(r)) {  // see k_mt_sync
@@ -3492,10 +3365,7 @@ __global__ __launch_bounds__(256) void k_export(KParams p, int64_t env, const ui
         else if (i == W) v = rew ? (uint32_t)rew[env] : 0u;
         else if (i == W + 1) v = done ? (uint32_t)done[env] : 0u;
         else if (i == W + 2 + ST_STAT_MT_INDEX) v = (uint32_t)idx;
-        else {
-            const int row = i - W - 2, hr = stat_hot_row(row);
-            v = hr >= 0 ? p.hot[(int64_t)hr * p.stride + env] : (uint32_t)p.cold[env * kCold + stat_cold_word(row)];
-        }
+        else v = (uint32_t)p.stats[(int64_t)(i - W - 2) * p.stride + env];
         out[i] = v;
     }
     if (parts & ST_EXPORT_MT) {
@@ -3849,35 +3719,6 @@ __global__ __launch_bounds__(256) void k_check_actions(const uint8_t *__restrict
     if (bad) flag[0] = 1u;
 }
 
-// ---------------------------------------------------------------- canonical rows
-// st_get_stats / st_set_stats: the ST_STAT_* rows [ST_NSTAT][stride] <-> the
-// hot rows and cold records (one env per thread); set recomputes the draw word
-__global__ __launch_bounds__(256) void k_get_stats(KParams p, int32_t *__restrict__ out) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= p.stride) return;
-    const int64_t sd = p.stride;
-#pragma unroll
-    for (int r = 0; r < ST_NSTAT; ++r) {
-        const int hr = stat_hot_row(r);
-        out[r * sd + e] = hr >= 0 ? (int32_t)p.hot[hr * sd + e] : p.cold[e * kCold + stat_cold_word(r)];
-    }
-}
-__global__ __launch_bounds__(256) void k_set_stats(KParams p, const int32_t *__restrict__ in) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= p.stride) return;
-    const int64_t sd = p.stride;
-    int32_t c[7];
-#pragma unroll
-    for (int r = 0; r < ST_NSTAT; ++r) {
-        const int32_t v = in[r * sd + e];
-        const int hr = stat_hot_row(r);
-        if (hr >= 0) p.hot[hr * sd + e] = (uint32_t)v;
-        else p.cold[e * kCold + stat_cold_word(r)] = v;
-        if (r >= ST_STAT_COUNT0 && r < ST_STAT_COUNT0 + 7) c[r - ST_STAT_COUNT0] = v;
-    }
-    p.hot[kHotDraw * sd + e] = dw_from_counts(c);
-}
-
 // ---------------------------------------------------------------- greedy policy
 // Benchmark / test workload generator (not part of the reference env): the
 // action a greedy placement player takes in every env's current state, so
@@ -4149,16 +3990,6 @@ hipError_t launch_policy_greedy(const KParams &p, uint64_t seed, int64_t t, uint
                                 uint8_t *out, hipStream_t s) {
     hipLaunchKernelGGL(k_policy_greedy, dim3((unsigned)(p.stride / kWave)), dim3(kWave), 0, s, p, seed, t,
                        explore, out);
-    return hipGetLastError();
-}
-
-hipError_t launch_get_stats(const KParams &p, int32_t *out, hipStream_t s) {
-    hipLaunchKernelGGL(k_get_stats, dim3((unsigned)((p.stride + 255) / 256)), dim3(256), 0, s, p, out);
-    return hipGetLastError();
-}
-
-hipError_t launch_set_stats(const KParams &p, const int32_t *in, hipStream_t s) {
-    hipLaunchKernelGGL(k_set_stats, dim3((unsigned)((p.stride + 255) / 256)), dim3(256), 0, s, p, in);
     return hipGetLastError();
 }
 

@@ -34,16 +34,12 @@ AUTORESET = {"none": 0, "same_step": 1}
 STAT = dict(time=0, score=1, lines=2, holes=3, piece_height=4, deaths=5, count0=6, mt_index=13,
             piece=14, ep_time=15, ep_score=16, ep_lines=17, ep_holes=18)
 NSTAT = 19
-# the hot rows and cold-record words of st_state_views (st_internal.h)
-HOT = dict(time=0, piece=1, mt=2, draw=3)
-NHOT, NCOLD = 4, 16
 MT_N = 624
 EXPORT_MT, EXPORT_OBS_F32 = 1, 2  # st_export_env parts
 
 EXPORTS = ("st_create", "st_destroy", "st_seed", "st_reset", "st_step", "st_step_f32", "st_step_vec", "st_rollout",
            "st_wire_words", "st_step_wire", "st_unwire", "st_unwire_shards",
-           "st_obs_to_f32", "st_render", "st_grayscale", "st_state", "st_get_stats", "st_set_stats", "st_copy",
-           "st_mt_sync", "st_state_bytes", "st_save",
+           "st_obs_to_f32", "st_render", "st_grayscale", "st_state", "st_copy", "st_mt_sync", "st_state_bytes", "st_save",
            "st_load", "st_export_env", "st_export_words", "st_check_actions", "st_set_action_flag", "st_stream_sync",
            "st_host_device_ptr", "st_gen_actions", "st_policy_greedy", "st_debug_stamps", "st_last_error", "st_abi_version")
 
@@ -64,7 +60,7 @@ class Config(ctypes.Structure):
 
 class StateViews(ctypes.Structure):
     _fields_ = [("board", ctypes.c_void_p), ("piece", ctypes.c_void_p),
-                ("hot", ctypes.c_void_p), ("cold", ctypes.c_void_p), ("mt", ctypes.c_void_p),
+                ("stats", ctypes.c_void_p), ("mt", ctypes.c_void_p),
                 ("n_envs", ctypes.c_int64), ("stride", ctypes.c_int64),
                 ("width", ctypes.c_int32), ("height", ctypes.c_int32),
                 ("mt_pitch", ctypes.c_int64)]
@@ -102,8 +98,6 @@ def load(path: str = LIB_PATH):
         "st_render": ([vp, vp, vp], ctypes.c_int),
         "st_grayscale": ([vp, vp, i32, i32, i32, vp, vp], ctypes.c_int),
         "st_state": ([vp, ctypes.POINTER(StateViews)], ctypes.c_int),
-        "st_get_stats": ([vp, vp, vp], ctypes.c_int),
-        "st_set_stats": ([vp, vp, vp], ctypes.c_int),
         "st_copy": ([vp, vp, i64, vp], ctypes.c_int),
         "st_mt_sync": ([vp, vp], ctypes.c_int),
         "st_state_bytes": ([vp], i64),
@@ -131,9 +125,9 @@ def load(path: str = LIB_PATH):
     if L.st_abi_version() != ABI_VERSION:
         if not ab_override:
             raise ImportError(f"libsimpletetris ABI {L.st_abi_version()} != {ABI_VERSION}")
-        # the state-view struct differs across ABIs: an older build serves
-        # raw ctypes A/Bs only (views read through the wrong struct size
-        # tensors from garbage)
+        # the state-view struct may differ across ABIs: an older build
+        # serves raw ctypes A/Bs only (views read through the wrong struct
+        # size tensors from garbage)
         L.st_state = None
     _lib = L
     return L

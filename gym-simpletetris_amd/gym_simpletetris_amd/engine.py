@@ -401,26 +401,20 @@ class TetrisBatch:
         with torch.cuda.device(self.device):
             C.check(self._L.st_mt_sync(self._ctx, self._stream()))
 
-    def state_tensors(self, fields=("board", "piece", "stats"), sync: bool = True, out: Optional[dict] = None) -> dict:
-        """Device copies of the state (full stride; slice [..., :n] for real envs):
-        board, piece and mt from the views, stats as the ST_STAT_* rows
-        (st_get_stats gathers them from the hot rows and cold records).
+    def state_tensors(self, fields=("board", "piece", "stats"), sync: bool = True) -> dict:
+        """Device copies of the state (full stride; slice [..., :n] for real envs).
         `sync=False` skips st_mt_sync: the MT index row then carries engine
-        bits (the counters are exact either way).  `out`: tensors to fill
-        (same shapes) instead of new ones."""
-        res = {}
+        bits (the counters are exact either way)."""
+        out = {}
         if sync and ("stats" in fields or "mt" in fields):
             self.sync_mt()
         s = self._stream()
-        for f in fields:  # st_copy / st_get_stats run on the stream's device: no device context needed
+        for f in fields:  # st_copy runs on the stream's device: no device context needed
             shape = self._sizes()[f]
-            t = out[f] if out is not None and f in out else torch.empty(shape, dtype=torch.int32, device=self.device)
-            if f == "stats":
-                C.check(self._L.st_get_stats(self._ctx, _ptr(t), s))
-            else:
-                C.check(self._L.st_copy(_ptr(t), ctypes.c_void_p(self._view_ptr(f)), t.numel() * 4, s))
-            res[f] = t
-        return res
+            t = torch.empty(shape, dtype=torch.int32, device=self.device)
+            C.check(self._L.st_copy(_ptr(t), ctypes.c_void_p(self._view_ptr(f)), t.numel() * 4, s))
+            out[f] = t
+        return out
 
     def get_state(self, fields=("board", "piece", "stats", "mt")) -> dict:
         """Host (numpy, uint32/int32) copy of the state of the real envs."""
@@ -438,7 +432,7 @@ class TetrisBatch:
         """Upload state arrays for the real envs (shapes as returned by
         get_state); padding envs keep their current state."""
         cur = self.state_tensors(tuple(fields))
-        # `piece` is also stats row 14: upload it after `stats`
+        # `piece` aliases stats row 14: upload it after `stats`
         order = sorted(fields, key=lambda f: ("stats", "board", "mt", "piece").index(f))
         with torch.cuda.device(self.device):
             for f in order:
@@ -450,11 +444,8 @@ class TetrisBatch:
                 else:
                     full[..., : self.n] = v
                 t = torch.from_numpy(full.view(np.int32)).to(self.device)
-                if f == "stats":  # scattered into the hot rows and cold records
-                    C.check(self._L.st_set_stats(self._ctx, _ptr(t), self._stream()))
-                else:
-                    C.check(self._L.st_copy(ctypes.c_void_p(self._view_ptr(f)), _ptr(t),
-                                            t.numel() * 4, self._stream()))
+                C.check(self._L.st_copy(ctypes.c_void_p(self._view_ptr(f)), _ptr(t),
+                                        t.numel() * 4, self._stream()))
             torch.cuda.synchronize(self.device)
 
     def save(self, path: Optional[str] = None) -> bytes:

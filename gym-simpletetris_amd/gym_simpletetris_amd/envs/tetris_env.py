@@ -160,7 +160,7 @@ class TetrisEnv:
         s = self._stream()
         C.check(L.st_copy(ctypes.c_void_p(v.mt), ctypes.c_void_p(self._h_mt.ctypes.data),
                           C.MT_N * 4, s))
-        C.check(L.st_copy(ctypes.c_void_p(v.hot + C.HOT["mt"] * v.stride * 4),  # the MT word (hot row)
+        C.check(L.st_copy(ctypes.c_void_p(v.stats + C.STAT["mt_index"] * v.stride * 4),
                           ctypes.c_void_p(self._h_idx.ctypes.data), 4, s))
         self._rng_sync_state = state  # the device now mirrors CPython's state
 

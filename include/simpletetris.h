@@ -32,9 +32,7 @@ extern "C" {
 #endif
 
 /* 2: st_step_wire carries the reward's 32 bits (st_wire_words grew by one
- * word for 10x20), st_unwire_shards; the state views describe the hot rows +
- * per-env cold records (st_state_views), the ST_STAT_* rows come and go
- * through st_get_stats / st_set_stats.  Snapshots (st_save) keep their own
+ * word for 10x20), st_unwire_shards.  Snapshots (st_save) keep their own
  * format version, unchanged. */
 #define ST_ABI_VERSION 2
 
@@ -104,29 +102,18 @@ enum st_stat {
  *   board  : uint32 [width][stride]  bit y of word (x, e) = board[x, y]
  *            (the reference's board[x, y], tetris_env.py:140, one bit-packed
  *            uint32 per board row x of the (width, height) array)
- *   hot    : uint32 [4][stride], what every env reads every step:
- *            row 0 time (int32), row 1 the piece word, row 2 the MT word
- *            (ST_STAT_MT_INDEX, see st_mt_sync), row 3 the draw word
- *            (engine-private: the shape counts' distances to their maximum,
- *            kept by the engine from the counts)
- *   piece  : uint32 [stride] = hot row 1:  id | rot<<3 | anchor_x<<5 |
- *            anchor_y<<11 | lock<<17; id in shape_names order T,J,L,Z,S,I,O
- *            (tetris_env.py:19); rot = number of rotate_left
- *            (rotated(cclk=False)) mod 4
- *   cold   : int32 [stride][16], one 64-byte record per env that only a lock
- *            reads and writes: score, lines, holes, piece_height, deaths,
- *            ep_time, ep_score, ep_lines, ep_holes, shape_counts[7]
+ *   piece  : uint32 [stride]  id | rot<<3 | anchor_x<<5 | anchor_y<<11 | lock<<17
+ *            (an alias of stats row ST_STAT_PIECE)
+ *            id in shape_names order T,J,L,Z,S,I,O (tetris_env.py:19);
+ *            rot = number of rotate_left (rotated(cclk=False)) mod 4
+ *   stats  : int32 [ST_NSTAT][stride]
  *   mt     : uint32 [stride][mt_pitch]; words [0, 624) of each row are the
  *            env's MT19937 state (CPython random.getstate()) after st_mt_sync;
- *            the rest is engine-private (the next generation, see st_mt_sync)
- * The counters as the ST_STAT_* rows of get_info: st_get_stats / st_set_stats
- * (writing the counts through the views directly would leave the draw word
- * stale: use st_set_stats). */
+ *            the rest is engine-private (the next generation, see st_mt_sync) */
 typedef struct st_state_views {
     uint32_t *board;
     uint32_t *piece;
-    uint32_t *hot;
-    int32_t *cold;
+    int32_t *stats;
     uint32_t *mt;
     int64_t n_envs;
     int64_t stride;
@@ -179,7 +166,7 @@ int st_step_f32(st_ctx *ctx, const uint8_t *d_actions, uint32_t *d_obs, float *d
  *     (ST_EINVAL otherwise).
  *   d_info (int32 [ST_NSTAT][n_envs], or NULL): every counter row after the
  *     step (get_info, :232-241, from one snapshot written by the step
- *     kernel): rows ST_STAT_* as st_get_stats returns them except
+ *     kernel): rows ST_STAT_* as in st_state_views.stats except
  *     ST_STAT_MT_INDEX (not written); the ST_STAT_EP_* rows hold the
  *     finished episode's counters where the env was reset in this step and
  *     0 elsewhere.
@@ -266,16 +253,6 @@ int st_export_words(int32_t width, int32_t height);
 /* Device views of the state (valid until st_destroy). */
 int st_state(st_ctx *ctx, st_state_views *out);
 
-/* The counters as rows: d_out int32 [ST_NSTAT][stride] (device), row r =
- * ST_STAT_r of every env (TetrisEngine's attributes, tetris_env.py:138-199;
- * ST_STAT_MT_INDEX as the engine keeps it: call st_mt_sync first for
- * CPython's index).  st_set_stats writes them back from d_in (same layout;
- * the engine's draw word is recomputed from the counts); ST_STAT_MT_INDEX
- * must then be CPython's form or a value st_get_stats returned.  Both on
- * `stream`, asynchronous. */
-int st_get_stats(st_ctx *ctx, int32_t *d_out, st_stream stream);
-int st_set_stats(st_ctx *ctx, const int32_t *d_in, st_stream stream);
-
 /* hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, stream) -- moves state
  * between the views above and caller buffers (crafted states). */
 int st_copy(void *dst, const void *src, int64_t bytes, st_stream stream);
@@ -288,9 +265,9 @@ int st_copy(void *dst, const void *src, int64_t bytes, st_stream stream);
  * current words may sit in the second buffer.  st_mt_sync (on `stream`)
  * brings every env back to CPython's form -- words [0, 624) of its mt row and
  * an index 0..624 equal random.getstate(), the preview's words given back.
- * Call it before reading the MT word (st_get_stats, hot row 2) or mt through
- * st_state's views; st_save calls it itself.  Writing a CPython state (words
- * [0, 624), index 0..624) is always valid. */
+ * Call it before reading stats or mt through st_state's views; st_save calls
+ * it itself.  Writing a CPython state (words [0, 624), index 0..624) is always
+ * valid. */
 int st_mt_sync(st_ctx *ctx, st_stream stream);
 
 /* State snapshot: the engine attributes of every env (board, piece, counters,

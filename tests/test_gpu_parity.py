@@ -877,7 +877,7 @@ def test_mt_generations_across_steps():
         raw = torch.empty(b.stride, dtype=torch.int32, device=b.device)
         v = b._views
         C.check(b._L.st_copy(ctypes.c_void_p(raw.data_ptr()),
-                             ctypes.c_void_p(v.hot + C.HOT["mt"] * v.stride * 4),
+                             ctypes.c_void_p(v.stats + C.STAT["mt_index"] * v.stride * 4),
                              raw.numel() * 4, b._stream()))
         saw_lazy |= bool((((raw[:n].cpu().numpy() >> 20) & 1) != 0).any())   # current generation in B
         if (c0 // chunk) % 3 == 1:
@@ -971,7 +971,7 @@ def test_preview_rewind_across_generations():
         assert np.array_equal(r.cpu().numpy(), ref["reward"][0]), t
         assert np.array_equal(o.cpu().numpy().view(np.uint32).T, ref["obs"][0]), t
         C.check(b._L.st_copy(ctypes.c_void_p(raw.data_ptr()),
-                             ctypes.c_void_p(v.hot + C.HOT["mt"] * v.stride * 4),
+                             ctypes.c_void_p(v.stats + C.STAT["mt_index"] * v.stride * 4),
                              raw.numel() * 4, b._stream()))
         w = raw[:n].cpu().numpy().astype(np.uint32)
         ok = ((w >> 24) & 1).astype(bool)
@@ -1248,10 +1248,9 @@ def test_host_written_large_shape_counts(mode):
     (tetris_env.py:183-191; Lib/random.py _randbelow).  The rollout's draw
     skips the tempering's last step only in waves whose lanes all draw <= 18
     bits: one wave here has none of the wide lanes, one only wide lanes, two
-    a mix.  The first wave's counts spread 14..17 apart: st_step's draw word
-    (nibble distances to the maximum, escaped past 15) crosses its escape
-    boundary both ways as shapes spawn.  Outputs and final counts / MT index
-    vs the oracle."""
+    a mix.  The first wave's counts spread 14..17 apart (the boundary of
+    round 5's measured-and-dropped draw word).  Outputs
+    and final counts / MT index vs the oracle."""
     G = _engine()
     n, T = 256, 80
     b = G.TetrisBatch(n, autoreset="same_step", seeds=range(n))
