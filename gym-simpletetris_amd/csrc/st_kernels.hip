@@ -181,7 +181,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uin
 // dependent launch's critical path (the guide's boundary cost + B / 6 TB/s);
 // `nt` stores stream out during the kernel instead (A/B, st_step packed:
 // 6.31 -> 5.89 us with obs, board, counter and MT stores all `nt`).
-constexpr int kNT = 2;
+// (A/B knob ST_STORE_CPOL: the gfx950 cache-policy bits of those stores --
+// 2 nt, 16 sc1, 18 sc1 + nt)
+#ifndef ST_STORE_CPOL
+#define ST_STORE_CPOL 2
+#endif
+constexpr int kNT = ST_STORE_CPOL;
 // Wave issue priorities (s_setprio), settled by A/B in rounds 1-3:
 // the draw wave after B1 at 2 (its chain was the critical one there: st_step
 // -1.5%, rollouts -6%; 0 / 1 / 3 re-checked in round 3 within noise,
