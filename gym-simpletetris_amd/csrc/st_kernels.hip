@@ -187,6 +187,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uin
 #define ST_STORE_CPOL 2
 #endif
 constexpr int kNT = ST_STORE_CPOL;
+// (A/B knob ST_STATE_CPOL: the policy of the state stores alone -- board,
+// counter rows, MT words -- which the next launch reads back; the outputs
+// keep kNT)
+#ifndef ST_STATE_CPOL
+#define ST_STATE_CPOL ST_STORE_CPOL
+#endif
+constexpr int kST = ST_STATE_CPOL;
 // Wave issue priorities (s_setprio), settled by A/B in rounds 1-3:
 // the draw wave after B1 at 2 (its chain was the critical one there: st_step
 // -1.5%, rollouts -6%; 0 / 1 / 3 re-checked in round 3 within noise,
@@ -1404,7 +1411,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         __builtin_amdgcn_raw_buffer_store_b32(
             (uint32_t)csid, rs,
             early_c && locknow && pv_ok(mt0) ? (uint32_t)e * 4u + (uint32_t)(ST_STAT_COUNT0 + pv_id(mt0)) * (uint32_t)sd * 4u
-                                             : kOff, 0, kNT);
+                                             : kOff, 0, kST);
     }
 
     // ---------------- logic: lock path (tetris_env.py:263-299) ----------------
@@ -1585,7 +1592,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         const uint32_t eo = (uint32_t)e * 4u;
         auto put = [&](int r, int32_t v, bool on) {
             __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, on ? eo + (uint32_t)r * (uint32_t)sd * 4u : kOff,
-                                                  0, kNT);
+                                                  0, kST);
         };
         // the finished episode's counters (ST_AUTORESET_SAME_STEP)
         put(ST_STAT_EP_TIME, time, reset_now);
@@ -1694,7 +1701,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 v.w &= km.w;
                 // row 4q + lrow; padding rows (>= W) are never dirty
                 const bool dirty = (ST_FULL_BOARD || ((bdl >> (4 * q)) & 1u)) && 4 * q + lrow < W && !(kAblate & 4096u);
-                buf_store16<kNT>(rb, dirty ? boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff, v);
+                buf_store16<kST>(rb, dirty ? boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff, v);
             }
         }
         // (below: the ragged / unaligned obs path and the float32 writer read
@@ -1746,7 +1753,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         // this step's next-generation chunk (its operands arrived long ago);
         // its env's progress advances unless that env's own draw switched
         // generations (finishing the successor itself: same words)
-        const int chunk_pg = mt_chunk_store<KSTEPS == 1 ? kNT : 0>(mrs, lane, chunk);
+        const int chunk_pg = mt_chunk_store<KSTEPS == 1 ? kST : 0>(mrs, lane, chunk);
         const bool chunk_me = lane == chunk.l;
         ST_STAMP(4);
         if constexpr (STAMP) {  // 1: a draw started a generation, 2: a draw ran past its 8 words
@@ -1780,18 +1787,18 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             const bool cst = !(kAblate & (2048u | 32768u));
             if constexpr (ST_FULL_DCNT && !VEC) {  // (A/B: every lane stores the count rows and the MT word)
                 __builtin_amdgcn_raw_buffer_store_b32(
-                    mt_out, rs, cst && real ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff, 0, kNT);
+                    mt_out, rs, cst && real ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff, 0, kST);
 #pragma unroll
                 for (int i = 0; i < 7; ++i)
                     __builtin_amdgcn_raw_buffer_store_b32(
                         dr && i == sid ? (uint32_t)csid : ss(ST_STAT_COUNT0 + i), rs,
-                        cst && real ? eo + (uint32_t)(ST_STAT_COUNT0 + i) * (uint32_t)sd * 4u : kOff, 0, kNT);
+                        cst && real ? eo + (uint32_t)(ST_STAT_COUNT0 + i) * (uint32_t)sd * 4u : kOff, 0, kST);
             } else {
             __builtin_amdgcn_raw_buffer_store_b32(
-                mt_out, rs, cst && !(kAblate & 131072u) && (dr || chunk_me) ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff, 0, kNT);
+                mt_out, rs, cst && !(kAblate & 131072u) && (dr || chunk_me) ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff, 0, kST);
             __builtin_amdgcn_raw_buffer_store_b32(
                 (uint32_t)csid, rs, cst && !(kAblate & 65536u) && dr && !(early_c && pv_ok(mt0))
-                                        ? eo + (uint32_t)(ST_STAT_COUNT0 + sid) * (uint32_t)sd * 4u : kOff, 0, kNT);
+                                        ? eo + (uint32_t)(ST_STAT_COUNT0 + sid) * (uint32_t)sd * 4u : kOff, 0, kST);
             }
             if constexpr (VEC) {  // st_step_vec's info snapshot: the shape counts after the step
                 const auto ri = buf_rsrc(p.info, (uint32_t)ST_NSTAT * (uint32_t)p.n * 4u);
@@ -1869,7 +1876,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             const uint32_t eo = (uint32_t)e * 4u;
             auto put = [&](int r, int32_t v, bool on) {
                 __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, on ? eo + (uint32_t)r * (uint32_t)sd * 4u : kOff,
-                                                      0, kNT);
+                                                      0, kST);
             };
             if constexpr (!ECNT) put(ST_STAT_TIME, time, true);
             put(kPieceRow, (int32_t)pw_out, true);
@@ -2076,7 +2083,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 v.y &= hmask;
                 v.z &= hmask;
                 v.w &= hmask;
-                buf_store16<kNT>(rb, boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u, v);
+                buf_store16<kST>(rb, boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u, v);
             }
         }
     }
@@ -2093,7 +2100,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         // row 15 (ep_time) is never staged: it is stored per lane on a reset
         if (((kOwn >> (4 * q)) & 0xFu) == 0u) continue;
         const bool st = (kOwn >> (4 * q + lrow)) & 1u;
-        buf_store16<kNT>(rs, st ? soff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff,
+        buf_store16<kST>(rs, st ? soff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff,
                          *reinterpret_cast<const uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]));
     }
     if constexpr (STAMP && KSTEPS != 1) {
@@ -2711,7 +2718,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 v.y &= hmask;
                 v.z &= hmask;
                 v.w &= hmask;
-                buf_store16<kNT>(rb, boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u, v);
+                buf_store16<kST>(rb, boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u, v);
             }
         }
     } else if constexpr (ROLE == kRoleD) {
@@ -3116,7 +3123,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
         for (int q = 0; q < kHotQ; ++q) {
             if (((kOwn >> (4 * q)) & 0xFu) == 0u) continue;
             const bool st = (kOwn >> (4 * q + lrow)) & 1u;
-            buf_store16<kNT>(rs, st ? soff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff,
+            buf_store16<kST>(rs, st ? soff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff,
                              *reinterpret_cast<const uint4 *>(&SS[(4 * q + lrow) * kWave + lcc]));
         }
     }
