@@ -228,6 +228,12 @@ constexpr int kLogicPrio = 1;
 #ifndef ST_RO_LDSWIN
 #define ST_RO_LDSWIN 0
 #endif
+// A/B knob (round 5): st_rollout's output wave consumes each MT chunk's
+// operand loads two steps after issuing them (one in-order vmcnt: a wait
+// for loads issued after a step's stores is also a wait for those stores)
+#ifndef ST_RO_CHLAG
+#define ST_RO_CHLAG 0
+#endif
 // A/B knob (round 5): st_step's logic wave stores its lock-path counters, the
 // episode rows of a reset and the clock right after the lock path, before the
 // obs / board store burst, instead of at the end of its chain
@@ -2940,14 +2946,27 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
         // computed and stored after the next step's obs stores: the loads have
         // a whole step to arrive, and the obs of a step never waits for them
         // (one in-order vmcnt: the wait covers only what was issued before)
-        [[maybe_unused]] MtChunk ch;
+        [[maybe_unused]] MtChunk ch, ch2;
         ch.l = -1;
+        ch2.l = -1;
+        // ST_RO_CHLAG: a chunk's operands consumed two steps after their
+        // issue instead of one (ch: the older chunk, ch2: the newer; a new
+        // chunk for the env the in-flight one serves starts past it)
+        constexpr bool LAG = ST_RO_CHLAG != 0;
         auto chunk_next = [&]() {
             const uint32_t w = sm.cw[lane];
             int pg = (int)(w & 0x3FFu);
             const int cur = (int)((w >> 10) & 1u);
             if (lane == last_l && cur == last_cur && last_pg > pg) pg = last_pg;
-            mt_chunk_issue_pc(orm, (w >> 31) != 0u && pg < kMtN, pg, cur, lane, ch);
+            if constexpr (LAG) {
+                if (lane == ch.l && cur == ch.cur) {
+                    const int pe = ch.pg + kWave < kMtN ? ch.pg + kWave : kMtN;
+                    pg = pe > pg ? pe : pg;
+                }
+                mt_chunk_issue_pc(orm, (w >> 31) != 0u && pg < kMtN, pg, cur, lane, ch2);
+            } else {
+                mt_chunk_issue_pc(orm, (w >> 31) != 0u && pg < kMtN, pg, cur, lane, ch);
+            }
         };
         auto chunk_done = [&]() {
             const int npg = mt_chunk_store<0>(orm, lane, ch);
@@ -3070,6 +3089,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                         }
                     }
                 }
+                stamp(3);
                 if constexpr (!EARLY) {
                     wave_sync();  // every read of the overlay plane precedes its clearing
     #pragma unroll
@@ -3099,8 +3119,11 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 }
                 if constexpr (!EARLY)
                     if (lane == 0) lds_flag_set(&sm.fq, (uint32_t)t + 1u);  // the logic wave may change the planes
+                stamp(4);
                 if constexpr (CHO) {
                     chunk_done();  // the previous step's (none at t = 0: ch.l < 0)
+                    stamp(5);
+                    if constexpr (LAG) ch = ch2;  // the in-flight one is next; ch2 takes a new one
                     chunk_next();
                 }
                 stamp(2);
@@ -3109,7 +3132,13 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
         if (!p.obs || (kAblate & 8u)) out_loop(std::integral_constant<int, 0>{});
         else if (wide_obs) out_loop(std::integral_constant<int, 1>{});
         else out_loop(std::integral_constant<int, 2>{});
-        if constexpr (CHO) chunk_done();
+        if constexpr (CHO) {
+            chunk_done();
+            if constexpr (LAG) {
+                ch = ch2;
+                chunk_done();
+            }
+        }
         wg_barrier();
     }
     // ---- counter rows this wave owns (logic: 0-5 and the piece row, draw:

@@ -33,7 +33,8 @@ LOGIC = [(1, "step start (action load)"), (2, "action + drop"), (3, "queue / pla
          (4, "lock path"), (5, "reward/done + mask"), (6, "obs planes + state")]
 DRAW = [(1, "round start"), (2, "chunk issue + mask wait"), (5, "draw"), (3, "ring + publish"),
         (6, "chunk bookkeeping"), (7, "window reload wait"), (4, "merge + reload issue")]
-OUT = [(1, "wait for the planes"), (2, "obs stores + clear")]
+OUT = [(1, "wait for the planes"), (3, "planes read + obs stores"), (4, "reward/done/ep stores"),
+       (5, "chunk: wait + twist + store"), (2, "next chunk issue")]
 res = []
 for c in range(NL):
     b.rollout(acts[c * CH:(c + 1) * CH], obs="packed", out=out)
