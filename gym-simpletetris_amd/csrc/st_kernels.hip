@@ -181,19 +181,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uin
 // dependent launch's critical path (the guide's boundary cost + B / 6 TB/s);
 // `nt` stores stream out during the kernel instead (A/B, st_step packed:
 // 6.31 -> 5.89 us with obs, board, counter and MT stores all `nt`).
-// (A/B knob ST_STORE_CPOL: the gfx950 cache-policy bits of those stores --
-// 2 nt, 16 sc1, 18 sc1 + nt)
-#ifndef ST_STORE_CPOL
-#define ST_STORE_CPOL 2
-#endif
-constexpr int kNT = ST_STORE_CPOL;
-// (A/B knob ST_STATE_CPOL: the policy of the state stores alone -- board,
-// counter rows, MT words -- which the next launch reads back; the outputs
-// keep kNT)
-#ifndef ST_STATE_CPOL
-#define ST_STATE_CPOL ST_STORE_CPOL
-#endif
-constexpr int kST = ST_STATE_CPOL;
+// (round 5, profiles/r05/ab_store_cache_policy.txt: `sc1` write-through
+// +12..15%, `sc1 nt` +15%; the state stores alone write-back or `sc0` +1..2%,
+// ab_state_store_cache_policy.txt)
+constexpr int kNT = 2;
+constexpr int kST = kNT;  // the state stores (board, counter rows, MT words)
 // Wave issue priorities (s_setprio), settled by A/B in rounds 1-3:
 // the draw wave after B1 at 2 (its chain was the critical one there: st_step
 // -1.5%, rollouts -6%; 0 / 1 / 3 re-checked in round 3 within noise,
@@ -202,44 +194,6 @@ constexpr int kST = ST_STATE_CPOL;
 // step: K = 2,000 4.67-4.72 -> 4.64-4.67 us, profiles/r03/ab_step_lprio.txt).
 constexpr int kDrawPrio = 2;
 constexpr int kLogicPrio = 1;
-// A/B knobs (round 5, partial-write study): store whole rows instead of the
-// changed 16-B groups / lanes only (same values, full lines written)
-#ifndef ST_FULL_BOARD
-#define ST_FULL_BOARD 0
-#endif
-#ifndef ST_FULL_LCNT
-#define ST_FULL_LCNT 0
-#endif
-#ifndef ST_FULL_DCNT
-#define ST_FULL_DCNT 0
-#endif
-// A/B knob (round 5): st_step's draw wave stores the spawned shape's count
-// right after B1 (known since the step started: the preview's shape) instead
-// of at the end of its chain (same-step auto-reset; lanes without a preview
-// keep the late store)
-#ifndef ST_EARLY_COUNT
-#define ST_EARLY_COUNT 0
-#endif
-// A/B knob (round 5): st_rollout's draw wave keeps each
-// lane's 16-word MT window in LDS (wb[j][lane]) instead of registers: the
-// words at the lane's offset are read by address (ds_read2st64) instead of
-// the 3-stage select network, and a reload is merged by LDS writes instead of
-// 16 register selects
-#ifndef ST_RO_LDSWIN
-#define ST_RO_LDSWIN 0
-#endif
-// A/B knob (round 5): st_rollout's output wave consumes each MT chunk's
-// operand loads two steps after issuing them (one in-order vmcnt: a wait
-// for loads issued after a step's stores is also a wait for those stores)
-#ifndef ST_RO_CHLAG
-#define ST_RO_CHLAG 0
-#endif
-// A/B knob (round 5): st_step's logic wave stores its lock-path counters, the
-// episode rows of a reset and the clock right after the lock path, before the
-// obs / board store burst, instead of at the end of its chain
-#ifndef ST_EARLY_CNT
-#define ST_EARLY_CNT 0
-#endif
 template <int AUX = 0>
 __device__ __forceinline__ void buf_store16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
     const i32x4 d = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
@@ -801,10 +755,9 @@ __device__ __forceinline__ int draw_shape(bool need, int32_t (&cnt)[7], uint32_t
 // getrandbits(k); lanes they do not settle continue from memory (draw_slow).
 // Same rule as draw_shape (randint(1, sum(m)), tetris_env.py:183-191); `mta`
 // (idx | pg | cur) and `o` advance past the words consumed.  Wave-uniform.
-template <bool FIN_ALL, bool LW = false>
+template <bool FIN_ALL>
 __device__ __forceinline__ int draw_win(bool need, const int32_t (&cnt)[7], uint32_t &mta, const MtPre &wv, int &o,
-                                        int wlim, uint32_t *mt_wave, uint32_t *S, int lane,
-                                        const uint32_t *wb = nullptr) {
+                                        int wlim, uint32_t *mt_wave, uint32_t *S, int lane) {
     int32_t maxc = cnt[0], sumc = cnt[0];
 #pragma unroll
     for (int i = 1; i < 7; ++i) {
@@ -827,25 +780,15 @@ __device__ __forceinline__ int draw_win(bool need, const int32_t (&cnt)[7], uint
         // reloaded after every draw, so o is the previous draw's few words;
         // o >= 8 takes the memory path)
         const int os = o & 7;
-        uint32_t w8[8];
-        if constexpr (LW) {
-            // the window in LDS, wb[j * 64 + lane]: the 8 words at os by
-            // address (bank = lane whatever the offset; ds_read2st64 pairs)
-            const uint32_t *w0 = wb + os * kWave + lane;
+        const uint32_t m4 = 0u - (uint32_t)((os >> 2) & 1), m2 = 0u - (uint32_t)((os >> 1) & 1);
+        const uint32_t m1 = 0u - (uint32_t)(os & 1);
+        uint32_t b[11], c[9], w8[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) w8[j] = w0[j * kWave];
-            (void)pick;
-        } else {
-            const uint32_t m4 = 0u - (uint32_t)((os >> 2) & 1), m2 = 0u - (uint32_t)((os >> 1) & 1);
-            const uint32_t m1 = 0u - (uint32_t)(os & 1);
-            uint32_t b[11], c[9];
+        for (int j = 0; j < 11; ++j) b[j] = pick(wv.w[j + 4], wv.w[j], m4);
 #pragma unroll
-            for (int j = 0; j < 11; ++j) b[j] = pick(wv.w[j + 4], wv.w[j], m4);
+        for (int j = 0; j < 9; ++j) c[j] = pick(b[j + 2], b[j], m2);
 #pragma unroll
-            for (int j = 0; j < 9; ++j) c[j] = pick(b[j + 2], b[j], m2);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) w8[j] = pick(c[j + 1], c[j], m1);
-        }
+        for (int j = 0; j < 8; ++j) w8[j] = pick(c[j + 1], c[j], m1);
         const int nv = o < 8 ? wlim - o : 0;  // valid words from o
         // words 0-3 tempered as independent chains (acceptance >= 1/2, ~0.7
         // typically: 4 rejections in a row are rare), 4-7 where a lane needs them
@@ -1356,7 +1299,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
 #pragma unroll
         for (int j = 0; j < 5; ++j)
             lcv[j] = __builtin_amdgcn_raw_buffer_load_b32(
-                rs, (ST_FULL_LCNT ? real : locknow) ? eo + (uint32_t)(ST_STAT_SCORE + j) * (uint32_t)sd * 4u : kOff,
+                rs, locknow ? eo + (uint32_t)(ST_STAT_SCORE + j) * (uint32_t)sd * 4u : kOff,
                 0, 0);
     }
     // the draw wave's next-generation chunk of this step: operands issued
@@ -1408,17 +1351,6 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     constexpr int kWin = STEP2 ? 8 : 16;
     MtPre pre;
     if constexpr (DO_D) mt_pre_load<kWin>(mrs, mtst, want_pre, pre);
-    // ST_EARLY_COUNT: the spawned shape's count, stored now (after the window
-    // loads are issued) where the spawn takes the preview
-    [[maybe_unused]] const bool early_c = ST_EARLY_COUNT && DO_D && STEP2 && !VEC &&
-                                          p.autoreset == ST_AUTORESET_SAME_STEP;
-    if constexpr (ST_EARLY_COUNT && DO_D && STEP2 && !VEC) {
-        const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
-        __builtin_amdgcn_raw_buffer_store_b32(
-            (uint32_t)csid, rs,
-            early_c && locknow && pv_ok(mt0) ? (uint32_t)e * 4u + (uint32_t)(ST_STAT_COUNT0 + pv_id(mt0)) * (uint32_t)sd * 4u
-                                             : kOff, 0, kST);
-    }
 
     // ---------------- logic: lock path (tetris_env.py:263-299) ----------------
     bool died = false, spawn = false;
@@ -1580,40 +1512,6 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         __builtin_amdgcn_raw_buffer_store_b32(rew, rr, real ? (uint32_t)e * 4u : kOff, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b8((char)(died ? 1 : 0), rd, real ? (uint32_t)e : kOff, 0, 0);
     }
-    // ECNT: the counters known after the lock path stored now (see ST_EARLY_CNT)
-    constexpr bool ECNT = ST_EARLY_CNT && DO_L && STEP2 && LCL && !VEC;
-    if constexpr (ECNT) {
-        if (locknow) {
-            o_score = (int32_t)lcv[0];
-            o_lines = (int32_t)lcv[1];
-            o_holes = (int32_t)lcv[2];
-            o_height = (int32_t)lcv[3];
-            o_deaths = (int32_t)lcv[4];
-            score += o_score;
-            lines += o_lines;
-            deaths += o_deaths;
-            if (!hset) height = o_height;
-        }
-        const auto rs = buf_rsrc(p.stats, (uint32_t)ST_NSTAT * (uint32_t)sd * 4u);
-        const uint32_t eo = (uint32_t)e * 4u;
-        auto put = [&](int r, int32_t v, bool on) {
-            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, on ? eo + (uint32_t)r * (uint32_t)sd * 4u : kOff,
-                                                  0, kST);
-        };
-        // the finished episode's counters (ST_AUTORESET_SAME_STEP)
-        put(ST_STAT_EP_TIME, time, reset_now);
-        put(ST_STAT_EP_SCORE, score, reset_now);
-        put(ST_STAT_EP_LINES, lines, reset_now);
-        put(ST_STAT_EP_HOLES, holes, reset_now);
-        if (reset_now) time = score = lines = holes = height = 0;
-        const bool cst = !(kAblate & (2048u | 16384u));
-        put(ST_STAT_TIME, time, true);
-        put(ST_STAT_SCORE, score, cst && locknow && score != o_score);
-        put(ST_STAT_LINES, lines, cst && locknow && lines != o_lines);
-        put(ST_STAT_HOLES, holes, cst && locknow && holes != o_holes);
-        put(ST_STAT_PIECE_HEIGHT, height, cst && locknow && height != o_height);
-        put(ST_STAT_DEATHS, deaths, cst && locknow && deaths != o_deaths);
-    }
     if constexpr (DO_L && KSTEPS == 1) {
         // The post-step board never depends on the spawned piece either (a
         // spawn only overlays row 0, which is empty after a non-fatal lock,
@@ -1706,7 +1604,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 v.z &= km.z;
                 v.w &= km.w;
                 // row 4q + lrow; padding rows (>= W) are never dirty
-                const bool dirty = (ST_FULL_BOARD || ((bdl >> (4 * q)) & 1u)) && 4 * q + lrow < W && !(kAblate & 4096u);
+                const bool dirty = ((bdl >> (4 * q)) & 1u) && 4 * q + lrow < W && !(kAblate & 4096u);
                 buf_store16<kST>(rb, dirty ? boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff, v);
             }
         }
@@ -1791,21 +1689,11 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             const uint32_t eo = (uint32_t)e * 4u;
             // (ablation 2048: the lock-path counter stores dropped, timing only)
             const bool cst = !(kAblate & (2048u | 32768u));
-            if constexpr (ST_FULL_DCNT && !VEC) {  // (A/B: every lane stores the count rows and the MT word)
-                __builtin_amdgcn_raw_buffer_store_b32(
-                    mt_out, rs, cst && real ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff, 0, kST);
-#pragma unroll
-                for (int i = 0; i < 7; ++i)
-                    __builtin_amdgcn_raw_buffer_store_b32(
-                        dr && i == sid ? (uint32_t)csid : ss(ST_STAT_COUNT0 + i), rs,
-                        cst && real ? eo + (uint32_t)(ST_STAT_COUNT0 + i) * (uint32_t)sd * 4u : kOff, 0, kST);
-            } else {
             __builtin_amdgcn_raw_buffer_store_b32(
                 mt_out, rs, cst && !(kAblate & 131072u) && (dr || chunk_me) ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff, 0, kST);
             __builtin_amdgcn_raw_buffer_store_b32(
-                (uint32_t)csid, rs, cst && !(kAblate & 65536u) && dr && !(early_c && pv_ok(mt0))
+                (uint32_t)csid, rs, cst && !(kAblate & 65536u) && dr
                                         ? eo + (uint32_t)(ST_STAT_COUNT0 + sid) * (uint32_t)sd * 4u : kOff, 0, kST);
-            }
             if constexpr (VEC) {  // st_step_vec's info snapshot: the shape counts after the step
                 const auto ri = buf_rsrc(p.info, (uint32_t)ST_NSTAT * (uint32_t)p.n * 4u);
 #pragma unroll
@@ -1840,10 +1728,10 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         }
 
         // ---- counters back to the staged rows (tetris_env.py:253, :264-299) ----
-        if constexpr (LCL && !ECNT) {
+        if constexpr (LCL) {
             // the late-loaded counters (issued before B1; the lock path kept
             // deltas) -- absolute values and the old ones for the dirty tests
-            if (ST_FULL_LCNT || locknow) {
+            if (locknow) {
                 o_score = (int32_t)lcv[0];
                 o_lines = (int32_t)lcv[1];
                 o_holes = (int32_t)lcv[2];
@@ -1864,7 +1752,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 ep_h = holes;
             }
         }
-        if (!ECNT && reset_now) {  // the finished episode's counters (ST_AUTORESET_SAME_STEP)
+        if (reset_now) {  // the finished episode's counters (ST_AUTORESET_SAME_STEP)
             int32_t *st = p.stats + e;
             st[ST_STAT_EP_TIME * sd] = time;
             st[ST_STAT_EP_SCORE * sd] = score;
@@ -1884,15 +1772,14 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, on ? eo + (uint32_t)r * (uint32_t)sd * 4u : kOff,
                                                       0, kST);
             };
-            if constexpr (!ECNT) put(ST_STAT_TIME, time, true);
+            put(ST_STAT_TIME, time, true);
             put(kPieceRow, (int32_t)pw_out, true);
-            const bool cst = !ECNT && !(kAblate & (2048u | 16384u));  // (ablation: lock-path counter stores dropped)
-            const bool fl = ST_FULL_LCNT && LCL && real;  // (A/B: every lane stores every row)
-            put(ST_STAT_SCORE, score, cst && (fl || (locknow && score != o_score)));
-            put(ST_STAT_LINES, lines, cst && (fl || (locknow && lines != o_lines)));
-            put(ST_STAT_HOLES, holes, cst && (fl || (locknow && holes != o_holes)));
-            put(ST_STAT_PIECE_HEIGHT, height, cst && (fl || (locknow && height != o_height)));
-            put(ST_STAT_DEATHS, deaths, cst && (fl || (locknow && deaths != o_deaths)));
+            const bool cst = !(kAblate & (2048u | 16384u));  // (ablation: lock-path counter stores dropped)
+            put(ST_STAT_SCORE, score, cst && locknow && score != o_score);
+            put(ST_STAT_LINES, lines, cst && locknow && lines != o_lines);
+            put(ST_STAT_HOLES, holes, cst && locknow && holes != o_holes);
+            put(ST_STAT_PIECE_HEIGHT, height, cst && locknow && height != o_height);
+            put(ST_STAT_DEATHS, deaths, cst && locknow && deaths != o_deaths);
             if constexpr (VEC) {
                 // st_step_vec's info snapshot: this wave's rows for every env
                 // (locking lanes from the registers, the others unchanged)
@@ -2222,7 +2109,6 @@ struct RoLds {
     // packed obs (the output wave builds the next-generation chunks):
     uint32_t cw[kWave];   // per lane: chunk candidate << 31 | cur << 10 | pg (draw -> output)
     uint32_t cpg[kWave];  // per lane: valid << 31 | cur << 10 | pg after a chunk (output -> draw)
-    uint32_t wb[ST_RO_LDSWIN ? kMtWin * kWave : 1];  // ST_RO_LDSWIN: the draw wave's MT windows [j][lane]
     uint32_t fl, fd, fo, fq;  // progress counters (see above)
 };
 // d[r] by selects on values (a select between two array elements would be
@@ -2756,11 +2642,6 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
         int o = 0, wlim = win_lim(mta), o_rl = 0, wlim_n = 0;
         mt_pre_load<kMtWin>(mrs, mta, real, win);
         mt_win_consume<kMtWin>(win);
-        constexpr bool LW = ST_RO_LDSWIN;
-        if constexpr (LW) {
-#pragma unroll
-            for (int j = 0; j < kMtWin; ++j) sm.wb[j * kWave + lane] = win.w[j];
-        }
         int q0 = pv_id(w0), q1;
         {
             // the queue's two pieces: q0 where the state has no preview
@@ -2768,14 +2649,14 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             // counts after q0's spawn
             const bool need1 = real && !pv_ok(w0);
             if (__ballot(need1)) {
-                const int pk = draw_win<CHO, LW>(need1, cnt_r, mta, win, o, wlim, mtg, sm.S, lane, sm.wb);
+                const int pk = draw_win<CHO>(need1, cnt_r, mta, win, o, wlim, mtg, sm.S, lane);
                 if (need1) q0 = pk;
             }
             int32_t cq[7];
 #pragma unroll
             for (int i = 0; i < 7; ++i) cq[i] = cnt_r[i] + (i == q0);
             const uint32_t m0 = mta;
-            q1 = draw_win<CHO, LW>(real, cq, mta, win, o, wlim, mtg, sm.S, lane, sm.wb);
+            q1 = draw_win<CHO>(real, cq, mta, win, o, wlim, mtg, sm.S, lane);
             c1 = mt_consumed(m0, mta);
         }
         int32_t cq[7];  // shape counts once the queue's head has spawned
@@ -2845,7 +2726,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 for (int i = 0; i < 7; ++i) cq[i] += (int32_t)((oh >> i) & 1u);
             }
             const uint32_t m0 = mta;
-            const int pk = draw_win<CHO, LW>(cons, cq, mta, win, o, wlim, mtg, sm.S, lane, sm.wb);
+            const int pk = draw_win<CHO>(cons, cq, mta, win, o, wlim, mtg, sm.S, lane);
             stamp(5);
             if (cons) {
                 q1 = pk;
@@ -2883,10 +2764,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             stamp(7);
             if (rl) {
 #pragma unroll
-                for (int j = 0; j < kMtWin; ++j) {
-                    if constexpr (LW) sm.wb[j * kWave + lane] = wn.w[j];
-                    else win.w[j] = wn.w[j];
-                }
+                for (int j = 0; j < kMtWin; ++j) win.w[j] = wn.w[j];
                 o -= o_rl;
                 wlim = wlim_n;
             }
@@ -2946,27 +2824,14 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
         // computed and stored after the next step's obs stores: the loads have
         // a whole step to arrive, and the obs of a step never waits for them
         // (one in-order vmcnt: the wait covers only what was issued before)
-        [[maybe_unused]] MtChunk ch, ch2;
+        [[maybe_unused]] MtChunk ch;
         ch.l = -1;
-        ch2.l = -1;
-        // ST_RO_CHLAG: a chunk's operands consumed two steps after their
-        // issue instead of one (ch: the older chunk, ch2: the newer; a new
-        // chunk for the env the in-flight one serves starts past it)
-        constexpr bool LAG = ST_RO_CHLAG != 0;
         auto chunk_next = [&]() {
             const uint32_t w = sm.cw[lane];
             int pg = (int)(w & 0x3FFu);
             const int cur = (int)((w >> 10) & 1u);
             if (lane == last_l && cur == last_cur && last_pg > pg) pg = last_pg;
-            if constexpr (LAG) {
-                if (lane == ch.l && cur == ch.cur) {
-                    const int pe = ch.pg + kWave < kMtN ? ch.pg + kWave : kMtN;
-                    pg = pe > pg ? pe : pg;
-                }
-                mt_chunk_issue_pc(orm, (w >> 31) != 0u && pg < kMtN, pg, cur, lane, ch2);
-            } else {
-                mt_chunk_issue_pc(orm, (w >> 31) != 0u && pg < kMtN, pg, cur, lane, ch);
-            }
+            mt_chunk_issue_pc(orm, (w >> 31) != 0u && pg < kMtN, pg, cur, lane, ch);
         };
         auto chunk_done = [&]() {
             const int npg = mt_chunk_store<0>(orm, lane, ch);
@@ -3123,7 +2988,6 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 if constexpr (CHO) {
                     chunk_done();  // the previous step's (none at t = 0: ch.l < 0)
                     stamp(5);
-                    if constexpr (LAG) ch = ch2;  // the in-flight one is next; ch2 takes a new one
                     chunk_next();
                 }
                 stamp(2);
@@ -3132,13 +2996,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
         if (!p.obs || (kAblate & 8u)) out_loop(std::integral_constant<int, 0>{});
         else if (wide_obs) out_loop(std::integral_constant<int, 1>{});
         else out_loop(std::integral_constant<int, 2>{});
-        if constexpr (CHO) {
-            chunk_done();
-            if constexpr (LAG) {
-                ch = ch2;
-                chunk_done();
-            }
-        }
+        if constexpr (CHO) chunk_done();
         wg_barrier();
     }
     // ---- counter rows this wave owns (logic: 0-5 and the piece row, draw:

@@ -300,22 +300,27 @@ class _Slot:
 
     def __init__(self, n, width, height, dev, f32, final):
         nd = (n + 3) // 4  # int32 words holding done's n bytes
-        rows = width + (width if final else 0) + C.NSTAT + 1
-        flat = torch.empty(rows * n + nd, dtype=torch.int32, device=dev)
+        wn = width * n
         # whole rows first: obs and the final obs start 16-B aligned whenever
-        # n % 4 == 0 (the step kernel's 16-B store path)
-        self.obs = flat[:width * n].view(width, n)
-        o = width * n
-        self.final = flat[o:o + width * n].view(width, n) if final else None
-        o += width * n if final else 0
-        self.info = flat[o:o + C.NSTAT * n].view(C.NSTAT, n)
-        o += C.NSTAT * n
-        self.reward = flat[o:o + n]
-        o += n
-        self.done = flat[o:o + nd].view(torch.uint8)[:n].view(torch.bool)
+        # n % 4 == 0 (the step kernel's 16-B store path); one split (a single
+        # op for all parts) and the kernel pointers by offset arithmetic --
+        # the per-step cost of copy=True is these Python-level tensor ops
+        sizes = (wn, wn, C.NSTAT * n, n, nd) if final else (wn, C.NSTAT * n, n, nd)
+        flat = torch.empty(sum(sizes), dtype=torch.int32, device=dev)
+        parts = flat.split(sizes)
+        self.obs = parts[0].view(width, n)
+        self.final = parts[1].view(width, n) if final else None
+        self.info = parts[-3].view(C.NSTAT, n)
+        self.reward = parts[-2]
+        self.done = parts[-1].view(torch.uint8)[:n].view(torch.bool)
         self.obs_f32 = torch.empty((n, width, height), dtype=torch.float32, device=dev) if f32 else None
-        self.ptrs = tuple(None if t is None else ctypes.c_void_p(t.data_ptr()) for t in
-                          (self.obs, self.obs_f32, self.reward, self.done, self.final, self.info))
+        base = flat.data_ptr()
+        offs = [0]
+        for z in sizes[:-1]:
+            offs.append(offs[-1] + 4 * z)
+        vp = ctypes.c_void_p
+        self.ptrs = (vp(base), None if self.obs_f32 is None else vp(self.obs_f32.data_ptr()), vp(base + offs[-2]),
+                     vp(base + offs[-1]), vp(base + offs[1]) if final else None, vp(base + offs[-3]))
         self.owner = None  # weakref to the VecInfo that reads this slot
 
 
