@@ -1115,12 +1115,18 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 bv[q] = *reinterpret_cast<const uint4 *>(bsrc + (size_t)(4 * q) * sd +
                                                          (4 * q + 4 <= W ? loff : clamp_off(q, W)));
     }
-    uint4 sv[kHotQ];
-#pragma unroll
-    for (int q = 0; q < kHotQ; ++q)
-        if (mine_q(q))
-            sv[q] = *reinterpret_cast<const uint4 *>(ssrc + (size_t)qbase(q) * sd +
-                                                     (qbase(q) + 4 <= kHotRows ? loff : clamp_off(q, kHotRows)));
+    // (four named registers, not an array: an array indexed in two unrolled
+    // loops was once left in scratch memory)
+    static_assert(kHotQ == 4, "four staged counter groups");
+    uint4 sv0 = make_uint4(0u, 0u, 0u, 0u), sv1 = sv0, sv2 = sv0, sv3 = sv0;
+    auto ldq = [&](int q) -> uint4 {
+        return *reinterpret_cast<const uint4 *>(ssrc + (size_t)qbase(q) * sd +
+                                                (qbase(q) + 4 <= kHotRows ? loff : clamp_off(q, kHotRows)));
+    };
+    if (mine_q(0)) sv0 = ldq(0);
+    if (mine_q(1)) sv1 = ldq(1);
+    if (mine_q(2)) sv2 = ldq(2);
+    if (mine_q(3)) sv3 = ldq(3);
     const int K = KSTEPS ? KSTEPS : p.k;
     // two-wave st_step: the logic wave also builds the next-generation block
     // (the draw wave's chain is the longer one).  (Measured and dropped: the
@@ -1198,9 +1204,11 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             }
         }
     }
-#pragma unroll
-    for (int q = 0; q < kHotQ; ++q)
-        if (mine_q(q)) *reinterpret_cast<uint4 *>(&SS[(qbase(q) + lrow) * kWave + lcc]) = sv[q];
+    auto stq = [&](int q, const uint4 &v) { *reinterpret_cast<uint4 *>(&SS[(qbase(q) + lrow) * kWave + lcc]) = v; };
+    if (mine_q(0)) stq(0, sv0);
+    if (mine_q(1)) stq(1, sv1);
+    if (mine_q(2)) stq(2, sv2);
+    if (mine_q(3)) stq(3, sv3);
     if constexpr (OVP && DO_L) {
 #pragma unroll
         for (int q = 0; q < NBQ; ++q)
@@ -2037,8 +2045,25 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
 }
 
 // st_step: two waves per 64 envs (kRoleL, kRoleD), see run_steps.
+// What the prologue's first loads address -- the state and action
+// pointers, the row stride, the env count -- comes as six leading scalar
+// arguments, preloaded into SGPRs at wave launch (gfx950 kernarg preload:
+// the Makefile builds with -mllvm -amdgpu-kernarg-preload-count=6; the
+// code object keeps the s_load fallback for firmware without it), so those
+// loads do not wait for a scalar load of the kernarg segment; the rest of
+// KParams arrives by s_load meanwhile, long before it is needed.  (Round 5
+// A/B, profiles/r05/ab_kernarg_preload.txt: C3 4.74 -> 4.62 us, C4 4.87 ->
+// 4.75 us per graph-replayed step.)
 template <int WT, int HT, bool F32, bool STAMP = false, bool SC0 = false, bool VEC = false>
-__global__ __launch_bounds__(2 * kWave) void k_step(KParams p) {
+__global__ __launch_bounds__(2 * kWave) void k_step(uint32_t *board, int32_t *stats, const uint8_t *actions,
+                                                    uint32_t *mt, int64_t stride, int64_t n, KParams p0) {
+    KParams p = p0;
+    p.board = board;
+    p.stats = stats;
+    p.actions = actions;
+    p.mt = mt;
+    p.stride = stride;
+    p.n = n;
     __shared__ StepLds<WT, F32, 1> sm;
     if (threadIdx.x < kWave) run_steps<WT, HT, F32, STAMP, 1, SC0, kRoleL, VEC>(p, sm);
     else run_steps<WT, HT, F32, STAMP, 1, SC0, kRoleD, VEC>(p, sm);
@@ -3714,32 +3739,34 @@ hipError_t launch_reset(const KParams &p, hipStream_t s) {
     return hipGetLastError();
 }
 
+// k_step's arguments: the preloaded six, then the whole KParams
+#define ST_STEP_ARGS(p) (p).board, (p).stats, (p).actions, (p).mt, (p).stride, (p).n, (p)
 hipError_t launch_step(const KParams &p, hipStream_t s) {
     const dim3 grid((unsigned)(p.stride / kWave)), block(2 * kWave);  // logic + draw wave
     const bool f32 = p.obs_f32 != nullptr;
     const bool sc0 = !(p.flags & kScoringFlags);
     if (p.final_obs || p.info) {  // st_step_vec: the vector env's outputs (VEC)
         if (p.W == 10 && p.H == 20) {
-            if (f32 && sc0) hipLaunchKernelGGL((k_step<10, 20, true, false, true, true>), grid, block, 0, s, p);
-            else if (f32) hipLaunchKernelGGL((k_step<10, 20, true, false, false, true>), grid, block, 0, s, p);
-            else if (sc0) hipLaunchKernelGGL((k_step<10, 20, false, false, true, true>), grid, block, 0, s, p);
-            else hipLaunchKernelGGL((k_step<10, 20, false, false, false, true>), grid, block, 0, s, p);
+            if (f32 && sc0) hipLaunchKernelGGL((k_step<10, 20, true, false, true, true>), grid, block, 0, s, ST_STEP_ARGS(p));
+            else if (f32) hipLaunchKernelGGL((k_step<10, 20, true, false, false, true>), grid, block, 0, s, ST_STEP_ARGS(p));
+            else if (sc0) hipLaunchKernelGGL((k_step<10, 20, false, false, true, true>), grid, block, 0, s, ST_STEP_ARGS(p));
+            else hipLaunchKernelGGL((k_step<10, 20, false, false, false, true>), grid, block, 0, s, ST_STEP_ARGS(p));
         } else {
-            if (f32) hipLaunchKernelGGL((k_step<0, 0, true, false, false, true>), grid, block, 0, s, p);
-            else hipLaunchKernelGGL((k_step<0, 0, false, false, false, true>), grid, block, 0, s, p);
+            if (f32) hipLaunchKernelGGL((k_step<0, 0, true, false, false, true>), grid, block, 0, s, ST_STEP_ARGS(p));
+            else hipLaunchKernelGGL((k_step<0, 0, false, false, false, true>), grid, block, 0, s, ST_STEP_ARGS(p));
         }
     } else if (p.stamps && p.W == 10 && p.H == 20) {
-        if (f32) hipLaunchKernelGGL((k_step<10, 20, true, true>), grid, block, 0, s, p);
-        else if (sc0) hipLaunchKernelGGL((k_step<10, 20, false, true, true>), grid, block, 0, s, p);
-        else hipLaunchKernelGGL((k_step<10, 20, false, true>), grid, block, 0, s, p);
+        if (f32) hipLaunchKernelGGL((k_step<10, 20, true, true>), grid, block, 0, s, ST_STEP_ARGS(p));
+        else if (sc0) hipLaunchKernelGGL((k_step<10, 20, false, true, true>), grid, block, 0, s, ST_STEP_ARGS(p));
+        else hipLaunchKernelGGL((k_step<10, 20, false, true>), grid, block, 0, s, ST_STEP_ARGS(p));
     } else if (p.W == 10 && p.H == 20) {
-        if (f32 && sc0) hipLaunchKernelGGL((k_step<10, 20, true, false, true>), grid, block, 0, s, p);
-        else if (f32) hipLaunchKernelGGL((k_step<10, 20, true>), grid, block, 0, s, p);
-        else if (sc0) hipLaunchKernelGGL((k_step<10, 20, false, false, true>), grid, block, 0, s, p);
-        else hipLaunchKernelGGL((k_step<10, 20, false>), grid, block, 0, s, p);
+        if (f32 && sc0) hipLaunchKernelGGL((k_step<10, 20, true, false, true>), grid, block, 0, s, ST_STEP_ARGS(p));
+        else if (f32) hipLaunchKernelGGL((k_step<10, 20, true>), grid, block, 0, s, ST_STEP_ARGS(p));
+        else if (sc0) hipLaunchKernelGGL((k_step<10, 20, false, false, true>), grid, block, 0, s, ST_STEP_ARGS(p));
+        else hipLaunchKernelGGL((k_step<10, 20, false>), grid, block, 0, s, ST_STEP_ARGS(p));
     } else {
-        if (f32) hipLaunchKernelGGL((k_step<0, 0, true>), grid, block, 0, s, p);
-        else hipLaunchKernelGGL((k_step<0, 0, false>), grid, block, 0, s, p);
+        if (f32) hipLaunchKernelGGL((k_step<0, 0, true>), grid, block, 0, s, ST_STEP_ARGS(p));
+        else hipLaunchKernelGGL((k_step<0, 0, false>), grid, block, 0, s, ST_STEP_ARGS(p));
     }
     return hipGetLastError();
 }
