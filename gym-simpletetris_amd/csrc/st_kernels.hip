@@ -186,6 +186,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uin
 // ab_state_store_cache_policy.txt)
 constexpr int kNT = 2;
 constexpr int kST = kNT;  // the state stores (board, counter rows, MT words)
+// the reward / done stores: nt like the obs (round 5 A/B against the
+// default policy, profiles/r05/ab_reward_done_nt.txt: -0.4..-0.9%)
+constexpr int kRD = kNT;
 // Wave issue priorities (s_setprio), settled by A/B in rounds 1-3:
 // the draw wave after B1 at 2 (its chain was the critical one there: st_step
 // -1.5%, rollouts -6%; 0 / 1 / 3 re-checked in round 3 within noise,
@@ -1517,8 +1520,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         // skipped on some path would make a later load's wait vmcnt(0).
         const auto rr = buf_rsrc(p.reward ? p.reward + (int64_t)t * p.n : nullptr, (uint32_t)p.n * 4u);
         const auto rd = buf_rsrc(p.done ? p.done + (int64_t)t * p.n : nullptr, (uint32_t)p.n);
-        __builtin_amdgcn_raw_buffer_store_b32(rew, rr, real ? (uint32_t)e * 4u : kOff, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b8((char)(died ? 1 : 0), rd, real ? (uint32_t)e : kOff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(rew, rr, real ? (uint32_t)e * 4u : kOff, 0, kRD);
+        __builtin_amdgcn_raw_buffer_store_b8((char)(died ? 1 : 0), rd, real ? (uint32_t)e : kOff, 0, kRD);
     }
     if constexpr (DO_L && KSTEPS == 1) {
         // The post-step board never depends on the spawned piece either (a
@@ -2995,8 +2998,8 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                     const auto rd = buf_rsrc(p.done ? p.done + (int64_t)t * p.n : nullptr, (uint32_t)p.n);
                     const uint32_t dn = sm.dn[t & 1][lane];
                     if (!(kAblate & 64u)) {
-                        __builtin_amdgcn_raw_buffer_store_b32(sm.rw[t & 1][lane], rr, real ? (uint32_t)e * 4u : kOff, 0, 0);
-                        __builtin_amdgcn_raw_buffer_store_b8((char)dn, rd, real ? (uint32_t)e : kOff, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b32(sm.rw[t & 1][lane], rr, real ? (uint32_t)e * 4u : kOff, 0, kRD);
+                        __builtin_amdgcn_raw_buffer_store_b8((char)dn, rd, real ? (uint32_t)e : kOff, 0, kRD);
                         const bool rs_now = dn != 0u && p.autoreset == ST_AUTORESET_SAME_STEP;
                         const auto rs = buf_rsrc(p.stats, (uint32_t)ST_NSTAT * (uint32_t)sd * 4u);
                         const uint32_t eo = (uint32_t)e * 4u;
