@@ -3007,7 +3007,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
 #pragma unroll
                         for (int k = 0; k < 4; ++k)
                             __builtin_amdgcn_raw_buffer_store_b32(sm.ep[t & 1][k][lane], rs,
-                                                                  rs_now ? eo + (uint32_t)kEpRow[k] * (uint32_t)sd * 4u : kOff, 0, 0);
+                                                                  rs_now ? eo + (uint32_t)kEpRow[k] * (uint32_t)sd * 4u : kOff, 0, kST);
                     }
                 }
                 if constexpr (!EARLY)
