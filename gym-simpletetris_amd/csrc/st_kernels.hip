@@ -2836,7 +2836,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
         // ================================================================ output
         const bool wide_obs = (p.n & 3) == 0 && e0 + kWave <= p.n && (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0;
         // packed obs: this wave builds the next-generation chunks (it idles
-        // most of each step), one per step, for the lowest lane the draw
+        // most of each step), one per two steps, for the lowest lane the draw
         // wave's cw word names; the new progress is published (cpg) right
         // after the chunk's stores are issued, and the wave's own last chunk
         // overrides a cw that does not show it yet.  A draw reads words past
@@ -2879,7 +2879,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             constexpr int OM = decltype(om_c)::value;  // 0: no packed obs, 1: 16-B rows, 2: one dword per row
             // (WT: the 16-B row groups read once per lane, compile-time rows)
             constexpr bool EARLY = OM == 1 && !F32 && WT != 0;
-            for (int t = 0; t < K; ++t) {
+            auto step_out = [&](int t, auto dn_c, auto nx_c) {
                 lds_flag_wait_ge(&sm.fo, (uint32_t)t + 1u);
                 stamp(1);
                 uint32_t *const obs_t = p.obs ? p.obs + (int64_t)t * W * p.n : nullptr;
@@ -3014,11 +3014,26 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                     if (lane == 0) lds_flag_set(&sm.fq, (uint32_t)t + 1u);  // the logic wave may change the planes
                 stamp(4);
                 if constexpr (CHO) {
-                    chunk_done();  // the previous step's (none at t = 0: ch.l < 0)
+                    if constexpr (decltype(dn_c)::value) chunk_done();  // the previous chunk (none at first: ch.l < 0)
                     stamp(5);
-                    chunk_next();
+                    if constexpr (decltype(nx_c)::value) chunk_next();
                 }
                 stamp(2);
+            };
+            if constexpr (CHO) {
+                // one chunk per two steps -- issued at even steps, computed
+                // and stored at odd ones (the unrolled pair keeps every vmcnt
+                // exact): 32 words per step and wave against the ~19 its 64
+                // envs' draws consume (p_lock 0.21 x ~1.4 words per draw);
+                // a chunk every step left the output wave's stores the
+                // step's bottleneck (round 5: 1.268 -> 1.24 us per step,
+                // profiles/r05/ab_rollout_chunk_every_other_step.txt)
+                for (int t = 0; t < K; t += 2) {
+                    step_out(t, std::false_type{}, std::true_type{});
+                    if (t + 1 < K) step_out(t + 1, std::true_type{}, std::false_type{});
+                }
+            } else {
+                for (int t = 0; t < K; ++t) step_out(t, std::true_type{}, std::true_type{});
             }
         };
         if (!p.obs || (kAblate & 8u)) out_loop(std::integral_constant<int, 0>{});
