@@ -2717,8 +2717,12 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             // the draw (the read's latency off this chain; a progress one
             // round staler only means a rarer, same-valued mt_finish)
             [[maybe_unused]] uint32_t cpgv = 0;
+            // the chunk bookkeeping (progress merge, candidacy) every other
+            // round: the output wave builds a chunk every other step (round
+            // 5: -1%, profiles/r05/ab_rollout_bookkeeping_every_other_round.txt)
+            [[maybe_unused]] const bool cwr = !(s & 1);
             if constexpr (CHO) {
-                cpgv = sm.cpg[lane];
+                if (cwr) cpgv = sm.cpg[lane];
             } else {
                 mt_chunk_issue(mrs, mta, real && ref_cur() == (int)((mta >> 20) & 1u) && !(kAblate & 16u), lane,
                                chunk);
@@ -2768,6 +2772,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             stamp(3);
             [[maybe_unused]] int chunk_pg = 0;
             if constexpr (CHO) {
+              if (cwr) {
                 // the progress, where the generation is still the one the
                 // chunk was built for
                 int ia, pga, ca;
@@ -2781,6 +2786,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 // incomplete
                 const bool cand = real && ref_cur() == ca && pga < kMtN && !(kAblate & 16u);
                 sm.cw[lane] = (cand ? 0x80000000u : 0u) | ((uint32_t)ca << 10) | (uint32_t)pga;
+              }
             } else {
                 chunk_pg = mt_chunk_store<0>(mrs, lane, chunk);
             }
