@@ -13,7 +13,7 @@ import gym_simpletetris_amd as G  # noqa: E402
 from gym_simpletetris_amd import _lib as C  # noqa: E402
 
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
-WU, n = 300, 65536
+WU, n = int(os.environ.get("AB_WU", "300")), 65536
 dev = torch.device("cuda", 0)
 s = torch.cuda.Stream(dev)
 sp = ctypes.c_void_p(s.cuda_stream)
