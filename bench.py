@@ -836,14 +836,10 @@ def main():
         variants = {}
         eng = head.eng
         L, ctx = eng._L, eng._ctx
-        def step_f32_variant():
-            if not f32:  # the same st_step with the reference's float32 obs fused in
-                w = Workload(args.n_envs, cfg_kw, True)
-                variants["step_f32"] = w.measure(steady=False)
-                w.close()
-        ro_first = os.environ.get("ST_BENCH_RO_FIRST") == "1"  # (diagnostic: variant order)
-        if not ro_first:
-            step_f32_variant()
+        if not f32:  # the same st_step with the reference's float32 obs fused in
+            w = Workload(args.n_envs, cfg_kw, True)
+            variants["step_f32"] = w.measure(steady=False)
+            w.close()
         # K-step rollout kernel (st_rollout), continuing the headline's state:
         # a fixed CH steps per launch whatever K is (so its PMC / trace keys
         # match the profiles' launch shape), max(5, K // CH) timed launches
@@ -878,8 +874,6 @@ def main():
                                       "p_lock": pl})}
             del rf
         del racts
-        if ro_first:
-            step_f32_variant()
         # the other single-GPU BASELINE configs: C2 (4,096 boards), C4 / C3
         other = "c3" if args.config == "c4" else "c4"
         w = Workload(args.n_envs, CONFIGS[other], f32)
