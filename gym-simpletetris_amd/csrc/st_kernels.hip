@@ -986,6 +986,16 @@ __device__ __forceinline__ void lds_flag_set(uint32_t *f, uint32_t v) {
     __hip_atomic_store((lds_u32 *)f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
+// The same without the release fence's lgkmcnt(0) wait: a wave's LDS
+// operations execute in issue order, so a flag stored after the data lands
+// after it (what lds_flag_get's readers rely on too).  The rollout's draw
+// wave publishes its queue counter this way (round 5: -1.7%,
+// profiles/r05/ab_rollout_queue_publish_nofence.txt).
+__device__ __forceinline__ void lds_flag_set_inorder(uint32_t *f, uint32_t v) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __hip_atomic_store((lds_u32 *)f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
 __device__ __forceinline__ void lds_flag_wait(uint32_t *f, uint32_t v) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     while (__hip_atomic_load((lds_u32 *)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != v)
@@ -2768,7 +2778,7 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                 nd += 1u;
             }
             lds_st(&sm.qring[lane], qw);
-            if (lane == 0) lds_flag_set(&sm.fd, (uint32_t)s + 2u);
+            if (lane == 0) lds_flag_set_inorder(&sm.fd, (uint32_t)s + 2u);
             stamp(3);
             [[maybe_unused]] int chunk_pg = 0;
             if constexpr (CHO) {
