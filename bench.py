@@ -888,6 +888,8 @@ def main():
                 pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 with torch.cuda.stream(s):
                     C.check(L.st_rollout(ctx, CH, aptr[0], *ptrs, sp))
+                    if os.environ.get("ST_BENCH_RO_PROBE_SYNC") == "1":
+                        sync_all()
                     pe0.record(s)
                     for c in range(1, 11):
                         C.check(L.st_rollout(ctx, CH, aptr[c % (nch + 1)], *ptrs, sp))
