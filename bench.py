@@ -49,7 +49,6 @@ KERNARG_FROM_ENV = bool(os.environ.get("HIP_FORCE_DEV_KERNARG"))
 if not KERNARG_FROM_ENV:
     os.environ["HIP_FORCE_DEV_KERNARG"] = "1"
 
-import numpy as np  # noqa: E402
 import torch  # noqa: E402  (importing torch does not initialise the GPU)
 import torch.distributed as dist  # noqa: E402
 
@@ -343,30 +342,26 @@ def main():
 
     pl_bufs = {}
 
-    def spawned_dev(eng, slot: int = 0):
-        """The envs' total spawn count (every lock spawns one piece): the seven
-        count rows copied on s into pinned host memory (slot `slot` of a
-        per-engine pair, allocated at the engine's first call --
-        Workload.__init__, before the warm-up), summed on the host later by
-        spawned_sum(eng, slot) once s has passed the copy.  No torch kernel
-        runs next to the timed region: a device reduction there (round 5's
-        first form) made the region's first st_step call cost ~20 us of host
-        time at its first use (profiles/r05/region_probe_*.jsonl), and even
-        warm it slowed the launches right after it (the rollout line 1.21 ->
-        1.30 us/step, profiles/r05/rollout_counter_read.txt)."""
+    def spawned_dev(eng, slot: int = 0) -> torch.Tensor:
+        """The envs' total spawn count (every lock spawns one piece) as a
+        device scalar in slot `slot` of a per-engine result pair, computed on
+        s (no host wait) into buffers allocated at the engine's first call --
+        Workload.__init__, before the warm-up: a device allocation (or a
+        torch kernel's first use) right before the timed region made its
+        first st_step call cost ~20 us of host time (profiles/r05/
+        region_probe_*.jsonl).  (A pinned-host copy summed on the host instead
+        measured 4% slower at the driver's K = 20 -- 1.17 against 1.22e10,
+        profiles/r05/ab_k20_counter_read.txt -- though it sped the rollout
+        line up 1.30 -> 1.27-1.30 us/step.)"""
         bufs = pl_bufs.get(id(eng))
         if bufs is None:
-            bufs = pl_bufs[id(eng)] = [torch.empty((7, eng.stride), dtype=torch.int32, pin_memory=True)
-                                       for _ in range(2)]
-        cnt = bufs[slot]
+            bufs = pl_bufs[id(eng)] = (torch.empty((7, eng.stride), dtype=torch.int32, device=dev),
+                                       torch.zeros(2, dtype=torch.int64, device=dev))
+        cnt, res = bufs
         src = eng._views.stats + C.STAT["count0"] * eng.stride * 4  # rows count0 .. count0 + 6
         C.check(eng._L.st_copy(ctypes.c_void_p(cnt.data_ptr()), ctypes.c_void_p(src), cnt.numel() * 4, sp))
-        return slot
-
-    def spawned_sum(eng, slot: int) -> int:
-        """The host sum of a copy spawned_dev(eng, slot) enqueued (s must have
-        passed it)."""
-        return int(pl_bufs[id(eng)][slot][:, :eng.n].numpy().sum(dtype=np.int64))
+        torch.sum(cnt[:, :eng.n], dim=(0, 1), dtype=torch.int64, out=res[slot])
+        return res[slot]
 
     def timed(eng, run, nsteps):
         """Time `run()` (enqueues exactly nsteps steps of `eng` on s): barrier +
@@ -394,10 +389,9 @@ def main():
             sync_all()
             t4 = time.perf_counter()
         elapsed = max_over_ranks(t4 - t0)
-        with torch.cuda.stream(s):  # (the second copy on s too, behind the region)
-            spawned_dev(eng, 1)
-        s.synchronize()
-        n_sp = spawned_sum(eng, 1) - spawned_sum(eng, c0)
+        with torch.cuda.stream(s):  # (the read on s too: c0 / c1 were computed there)
+            c1 = spawned_dev(eng, 1)
+            n_sp = int((c1 - c0).item())
         if DEBUG:
             print("timed: rec0 %.1f run %.1f rec1 %.1f sync %.1f us" % ((t1 - t0) * 1e6, (t2 - t1) * 1e6,
                   (t3 - t2) * 1e6, (t4 - t3) * 1e6), file=sys.stderr)
