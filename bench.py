@@ -860,13 +860,27 @@ def main():
             aptr = [ctypes.c_void_p(racts[c * CH].data_ptr()) for c in range(nch + 1)]
             ptrs = [ctypes.c_void_p(x.data_ptr()) if x is not None else None for x in (ro, rf, rr, rd)]
 
+            per_launch = os.environ.get("ST_BENCH_RO_PERLAUNCH") == "1" and not use_f32
+            pev = [torch.cuda.Event(enable_timing=True) for _ in range(nch + 1)] if per_launch else None
+            if per_launch:
+                with torch.cuda.stream(s):
+                    for e in pev:
+                        e.record(s)
+
             def run_ro():
+                if per_launch:  # (diagnostic) an event behind every launch of the region
+                    pev[0].record(s)
                 for c in range(1, nch + 1):
                     C.check(L.st_rollout(ctx, CH, aptr[c], *ptrs, sp))
+                    if per_launch:
+                        pev[c].record(s)
             with torch.cuda.stream(s):  # warm-up launch (timed() waits for it before reading counters)
                 C.check(L.st_rollout(ctx, CH, aptr[0], *ptrs, sp))
             el, ev, pl = timed(eng, run_ro, nch * CH)
             ev_us = ev * 1e3 / nch
+            if per_launch:
+                print("ro_per_launch us/step " + " ".join("%.3f" % (pev[c - 1].elapsed_time(pev[c]) * 1e3 / CH)
+                                                        for c in range(1, nch + 1)), file=sys.stderr)
             variants["rollout_f32" if use_f32 else "rollout_packed"] = {
                 "value": head.n_global * nch * CH / el, "ms_per_step": el / (nch * CH) * 1e3,
                 "steps_per_launch": CH, "launches": nch, "p_lock": pl,
