@@ -970,29 +970,42 @@ def vec_env_variant(n: int, steps: int, dev):
     check, with the step kernel's own check ('async', the default: a sticky
     flag in mapped host memory, st_set_action_flag; no extra launch, no sync)
     and with the per-step device->host check (True); copy=True (default)
-    and, with 'async', copy=False."""
+    and, with 'async', copy=False, and copy=True with every step's outputs
+    kept for 8 steps (`/held8`: no slot is free to reuse)."""
     from gym_simpletetris_amd.envs.tetris_env import TetrisVecEnv
     out = {}
     for fmt in ("packed", "f32"):
-        for val, cp in ((False, True), ("async", True), (True, True), ("async", False)):
+        for val, cp, hold in ((False, True, 0), ("async", True, 0), (True, True, 0), ("async", False, 0),
+                              ("async", True, 8)):
             v = TetrisVecEnv(n, seed=1000, obs_format=fmt, validate_actions=val, device=dev, copy=cp)
             v.reset()
             acts = torch.randint(0, 7, (64, n), dtype=torch.uint8, device=dev)
+            ring = [None] * max(hold, 1)
             for t in range(50):
-                v.step(acts[t % 64])
+                ring[t % len(ring)] = v.step(acts[t % 64]) if hold else None
             torch.cuda.synchronize(dev)
+            r0 = v.slots_reused
             t0 = time.perf_counter()
-            for t in range(steps):
-                v.step(acts[t % 64])
+            if hold:
+                for t in range(steps):
+                    ring[t % hold] = v.step(acts[t % 64])
+            else:
+                for t in range(steps):
+                    v.step(acts[t % 64])
             torch.cuda.synchronize(dev)
             dt = (time.perf_counter() - t0) / steps
-            key = f"{fmt}/validate_actions={val}" + ("" if cp else "/copy=False")
+            key = f"{fmt}/validate_actions={val}" + ("" if cp else "/copy=False") + (f"/held{hold}" if hold else "")
             out[key] = {"us_per_step": dt * 1e6, "env_steps_per_s": n / dt}
+            if cp:
+                out[key]["slots_reused"] = v.slots_reused - r0
+            del ring
             v.close()
     out["note"] = ("TetrisVecEnv.step incl. the per-step info snapshot; copy=True (the default): every "
-                   "step's outputs in tensors allocated for it (the caller's to keep); copy=False: two "
-                   "alternating output slots (overwritten two steps later); host-bound above the kernel "
-                   "(DESIGN.md §5.1)")
+                   "step's outputs in tensors of their own, never written again while the caller holds "
+                   "any of them (a recent step's slot is reused once nothing of it is referenced: "
+                   "slots_reused); copy=False: two alternating output slots (overwritten two steps "
+                   "later); held8: copy=True with each step's outputs kept 8 steps; host-bound above the "
+                   "kernel (DESIGN.md §5.1)")
     return out
 
 

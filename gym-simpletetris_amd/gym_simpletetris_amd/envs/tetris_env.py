@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes
 import random
+import sys
 import weakref
 from typing import Optional
 
@@ -291,37 +292,71 @@ class TetrisEnv:
             self.engine = None
 
 
+class _SlotLayout:
+    """The part sizes and byte offsets of a vector env's output slot,
+    computed once per env (every slot of it has the same layout)."""
+
+    def __init__(self, n, width, height, f32, final):
+        nd = (n + 3) // 4  # int32 words holding done's n bytes
+        wn = width * n
+        # whole rows first: obs and the final obs start 16-B aligned whenever
+        # n % 4 == 0 (the step kernel's 16-B store path)
+        self.sizes = (wn, wn, C.NSTAT * n, n, nd) if final else (wn, C.NSTAT * n, n, nd)
+        self.total = sum(self.sizes)
+        offs = [0]
+        for z in self.sizes[:-1]:
+            offs.append(offs[-1] + 4 * z)
+        self.offs = tuple(offs)
+        self.n, self.width, self.height, self.f32, self.final = n, width, height, f32, final
+
+
 class _Slot:
     """One set of st_step_vec outputs: with copy=False the vector env
     alternates two; with copy=True every step gets a fresh one, handed to
     the caller (the env never writes it again).  The int32 outputs are views
-    of ONE allocation (obs | reward | done bytes | final obs | info rows), the
-    float32 obs a second one: two caching-allocator calls per step."""
+    of ONE allocation (obs | final obs | info rows | reward | done bytes),
+    the float32 obs a second one: two caching-allocator calls per step.  The
+    per-step cost of copy=True is these Python-level tensor ops, so only the
+    returned obs / reward / done are viewed here; the info rows and the
+    final obs are viewed when an info is read (VecInfo)."""
 
-    def __init__(self, n, width, height, dev, f32, final):
-        nd = (n + 3) // 4  # int32 words holding done's n bytes
-        wn = width * n
-        # whole rows first: obs and the final obs start 16-B aligned whenever
-        # n % 4 == 0 (the step kernel's 16-B store path); one split (a single
-        # op for all parts) and the kernel pointers by offset arithmetic --
-        # the per-step cost of copy=True is these Python-level tensor ops
-        sizes = (wn, wn, C.NSTAT * n, n, nd) if final else (wn, C.NSTAT * n, n, nd)
-        flat = torch.empty(sum(sizes), dtype=torch.int32, device=dev)
-        parts = flat.split(sizes)
-        self.obs = parts[0].view(width, n)
-        self.final = parts[1].view(width, n) if final else None
-        self.info = parts[-3].view(C.NSTAT, n)
+    def __init__(self, lay: _SlotLayout, dev):
+        n = lay.n
+        self.lay = lay
+        flat = torch.empty(lay.total, dtype=torch.int32, device=dev)
+        self.parts = parts = flat.split(lay.sizes)  # one op for every part
+        self.obs = parts[0].view(lay.width, n)
         self.reward = parts[-2]
         self.done = parts[-1].view(torch.uint8)[:n].view(torch.bool)
-        self.obs_f32 = torch.empty((n, width, height), dtype=torch.float32, device=dev) if f32 else None
-        base = flat.data_ptr()
-        offs = [0]
-        for z in sizes[:-1]:
-            offs.append(offs[-1] + 4 * z)
+        self.obs_f32 = torch.empty((n, lay.width, lay.height), dtype=torch.float32, device=dev) if lay.f32 else None
+        base, o = flat.data_ptr(), lay.offs
         vp = ctypes.c_void_p
-        self.ptrs = (vp(base), None if self.obs_f32 is None else vp(self.obs_f32.data_ptr()), vp(base + offs[-2]),
-                     vp(base + offs[-1]), vp(base + offs[1]) if final else None, vp(base + offs[-3]))
+        self.ptrs = (vp(base), None if self.obs_f32 is None else vp(self.obs_f32.data_ptr()), vp(base + o[-2]),
+                     vp(base + o[-1]), vp(base + o[1]) if lay.final else None, vp(base + o[-3]))
         self.owner = None  # weakref to the VecInfo that reads this slot
+        self._flat_st = flat.untyped_storage()
+        self._f32_st = self.obs_f32.untyped_storage() if self.obs_f32 is not None else None
+        self._idle = self._refs()  # the counts while only the slot holds its tensors
+
+    def _refs(self):
+        """Python references to the tensors step() hands out, and the owners
+        of the two allocations (every view of them, the caller's included)."""
+        f32 = self.obs_f32 is not None  # (None's own count moves all the time: not counted)
+        return (sys.getrefcount(self.obs), sys.getrefcount(self.reward), sys.getrefcount(self.done),
+                sys.getrefcount(self.obs_f32) if f32 else 0, torch._C._storage_Use_Count(self._flat_st._cdata),
+                torch._C._storage_Use_Count(self._f32_st._cdata) if f32 else 0)
+
+    def idle(self) -> bool:
+        """Nothing outside the slot still holds its outputs (no returned
+        tensor, view of one, info or info tensor): a copy=True env may write
+        the next step into it without touching anything the caller kept."""
+        return self._refs() == self._idle
+
+    def info_rows(self):
+        return self.parts[-3].view(C.NSTAT, self.lay.n)
+
+    def final_obs(self):
+        return self.parts[1].view(self.lay.width, self.lay.n) if self.lay.final else None
 
 
 class VecInfo:
@@ -344,14 +379,22 @@ class VecInfo:
 
     def __init__(self, env: "TetrisVecEnv", slot: _Slot):
         self._env = env
-        self._info, self._final, self._done = slot.info, slot.final, slot.done
+        self._slot = slot  # the info rows / final obs are viewed on first access
+        self._info = self._final = None
+        self._done = slot.done
         self._cache = None
+
+    def _views(self):
+        if self._slot is not None:
+            self._info, self._final = self._slot.info_rows(), self._slot.final_obs()
+            self._slot = None
 
     def _detach(self):
         """Own copies of the slot's tensors (the env is about to reuse it;
         stream-ordered before the step that overwrites it).  A dict already
         built from the slot is rebuilt from the copies on the next access
         (its counter tensors were views into the slot)."""
+        self._views()
         self._info = self._info.clone()
         self._done = self._done.clone()
         if self._final is not None:
@@ -360,6 +403,7 @@ class VecInfo:
 
     def _load(self):
         if self._cache is None:
+            self._views()
             env = self._env
             d = env.engine.info_tensors(self._info)
             d["current_piece"] = self._info[C.STAT["piece"]] & 7
@@ -409,9 +453,11 @@ class TetrisVecEnv:
     obs, reward, done, the terminal obs and the info counters.  copy=True
     (default; gym's SyncVectorEnv convention, and the reference's step
     returns a fresh np.copy of the board, tetris_env.py:302): the kernel
-    writes them into tensors allocated for this step, which the env never
-    touches again -- obs / reward / done / info stay valid as long as the
-    caller keeps them.  copy=False: they live in one of two output slots
+    writes them into tensors of their own, which the env never touches
+    again while the caller keeps any of them -- obs / reward / done / info,
+    a view of one, an info tensor (a slot of the last few steps is reused
+    once none of that is referenced any more, when torch's allocator would
+    hand the memory out again: `slots_reused` counts those steps).  copy=False: they live in one of two output slots
     that alternate, so they are overwritten two steps later (an info object
     kept longer takes a copy; the obs / reward / done tensors do not) -- the
     fast path, for loops that consume each step's outputs right away.
@@ -462,10 +508,18 @@ class TetrisVecEnv:
         fin = self.autoreset and autoreset_obs == "reset"
         self.copy = bool(copy)
         self._fin = fin
-        self._slots = [] if self.copy else \
-            [_Slot(self.num_envs, width, height, self.device, self._want_f32, fin) for _ in range(2)]
+        self._lay = _SlotLayout(self.num_envs, width, height, self._want_f32, fin)
+        self._slots = [] if self.copy else [_Slot(self._lay, self.device) for _ in range(2)]
+        # copy=True: the last few steps' slots, reused once the caller holds
+        # nothing of them (_Slot.idle) -- an RL loop that drops each step's
+        # outputs then pays no allocation per step; one that keeps them gets
+        # fresh slots, and the pool forgets the oldest
+        self._pool: list = []
+        self.slots_reused = 0
         self._k = 0
         self._step_vec = self.engine._L.st_step_vec
+
+    _POOL = 4  # copy=True: slots kept for reuse
 
     def _obs(self, packed, f32):
         if self.obs_format == "packed":
@@ -502,7 +556,17 @@ class TetrisVecEnv:
         eng = self.engine
         a = eng._actions(actions)
         if self.copy:  # this step's outputs, the caller's from now on
-            slot = _Slot(self.num_envs, self.width, self.height, self.device, self._want_f32, self._fin)
+            slot = None
+            for i, z in enumerate(self._pool):
+                if z.idle():
+                    slot = self._pool.pop(i)
+                    self.slots_reused += 1
+                    break
+            if slot is None:
+                slot = _Slot(self._lay, self.device)
+                if len(self._pool) >= self._POOL:
+                    self._pool.pop(0)  # still the caller's: it is freed when they drop it
+            self._pool.append(slot)
         else:
             slot = self._slots[self._k]
             self._k ^= 1

@@ -202,6 +202,43 @@ def test_vec_env_outputs_kept_across_steps(obs_format):
     u.close()
 
 
+@pytest.mark.parametrize("obs_format", ["packed", "f32"])
+def test_vec_env_copy_reuses_only_dropped_slots(obs_format):
+    """copy=True reuses a recent step's output slot once nothing of it is
+    referenced (an RL loop that drops each step's outputs allocates nothing
+    per step), and never one the caller still holds in any form: a derived
+    view of the obs, the reward tensor, an info tensor, the info itself.
+    Every step's outputs equal a copy=False twin's, and the held pieces are
+    unchanged ten steps later."""
+    G = _engine()
+    n = 2048
+    v = G.TetrisVecEnv(n, seed=13, obs_format=obs_format)
+    u = G.TetrisVecEnv(n, seed=13, obs_format=obs_format, copy=False)
+    v.reset()
+    u.reset()
+    held = {}
+    for t in range(60):
+        acts = v.engine.gen_actions(t, 9).clone()
+        ov, rv, dv, iv = v.step(acts)
+        ou, ru, du, iu = u.step(acts)
+        assert torch.equal(ov, ou) and torch.equal(rv, ru) and torch.equal(dv, du), t
+        assert torch.equal(iv["score"], iu["score"]) and torch.equal(iv["final_observation"], iu["final_observation"]), t
+        k = t % 5
+        if t in (10, 20, 30, 40):  # keep one piece of this step's outputs, drop the rest
+            piece = {10: ov[..., :7], 20: rv, 30: iv["lines_cleared"], 40: iv}[t]
+            want = {10: ou[..., :7], 20: ru, 30: iu["lines_cleared"], 40: iu["time"]}[t].clone()
+            held[t] = (piece, want)
+        del ov, rv, dv, iv
+        for t0, (piece, want) in held.items():
+            got = piece["time"] if t0 == 40 else piece
+            assert torch.equal(got, want), (t0, t)
+        del k
+    # the drop-everything steps ran on recycled slots
+    assert v.slots_reused >= 60 - 4 - 8, v.slots_reused
+    v.close()
+    u.close()
+
+
 def test_vec_env_reset_return_info_vs_oracle():
     """reset(return_info=True) (tetris_env.py:405-411): (obs, info) with the
     post-clear() counters -- time / score / lines / holes / piece_height 0,
