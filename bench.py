@@ -860,7 +860,7 @@ def main():
             aptr = [ctypes.c_void_p(racts[c * CH].data_ptr()) for c in range(nch + 1)]
             ptrs = [ctypes.c_void_p(x.data_ptr()) if x is not None else None for x in (ro, rf, rr, rd)]
 
-            per_launch = os.environ.get("ST_BENCH_RO_PERLAUNCH") == "1" and not use_f32
+            per_launch = os.environ.get("ST_BENCH_RO_PERLAUNCH") == "1"
             pev = [torch.cuda.Event(enable_timing=True) for _ in range(nch + 1)] if per_launch else None
             if per_launch:
                 with torch.cuda.stream(s):
@@ -879,7 +879,7 @@ def main():
             el, ev, pl = timed(eng, run_ro, nch * CH)
             ev_us = ev * 1e3 / nch
             if per_launch:
-                print("ro_per_launch us/step " + " ".join("%.3f" % (pev[c - 1].elapsed_time(pev[c]) * 1e3 / CH)
+                print(("ro_per_launch f32" if use_f32 else "ro_per_launch") + " us/step " + " ".join("%.3f" % (pev[c - 1].elapsed_time(pev[c]) * 1e3 / CH)
                                                         for c in range(1, nch + 1)), file=sys.stderr)
             variants["rollout_f32" if use_f32 else "rollout_packed"] = {
                 "value": head.n_global * nch * CH / el, "ms_per_step": el / (nch * CH) * 1e3,
