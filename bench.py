@@ -229,6 +229,46 @@ def cpu_baseline(seconds: float, config: str):
 
 
 # ----------------------------------------------------------------------------- launcher
+def rank_topology(dev, rank: int, local_rank: int, world: int, use_dist: bool, backend: str) -> dict:
+    """This rank's device identity (index, name, UUID / PCI ids where torch
+    exposes them), all-gathered over the process group when there is one:
+    ranks_seen = the identities received, distinct_devices = the distinct
+    physical GPUs among them (UUID, else PCI domain:bus:device, else host +
+    visible-device list + index), and the RCCL version the nccl backend
+    loaded."""
+    import socket
+    p = torch.cuda.get_device_properties(dev)
+    ident = {"rank": rank, "local_rank": local_rank, "device_index": dev.index, "name": p.name,
+             "host": socket.gethostname()}
+    for k in ("uuid", "pci_domain_id", "pci_bus_id", "pci_device_id"):
+        v = getattr(p, k, None)
+        if v is not None:
+            ident[k] = str(v)
+    vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES") \
+        or os.environ.get("CUDA_VISIBLE_DEVICES")
+    if "uuid" in ident:
+        key = "uuid:" + ident["uuid"]
+    elif "pci_bus_id" in ident:
+        key = "pci:%s:%s:%s" % (ident["host"], ident.get("pci_domain_id"), ident["pci_bus_id"]) \
+            + ":%s" % ident.get("pci_device_id")
+    else:
+        key = "idx:%s:%s:%s" % (ident["host"], vis, dev.index)
+    ident["device_key"] = key
+    devices = [ident]
+    if use_dist:
+        devices = [None] * world
+        dist.all_gather_object(devices, ident)
+    rccl = None
+    if backend == "nccl" and use_dist:
+        try:
+            v = torch.cuda.nccl.version()
+            rccl = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+        except Exception as ex:  # noqa: BLE001 (reported, not fatal)
+            rccl = f"unknown ({ex})"
+    return {"ranks_seen": len(devices), "distinct_devices": len({d["device_key"] for d in devices}),
+            "backend": backend if use_dist else None, "rccl_version": rccl, "devices": devices}
+
+
 def spawn_ranks(n: int) -> int:
     """`bench.py --gpus N` run directly: start N rank processes (this parent
     never touches a GPU), rendezvous on 127.0.0.1, return the worst exit code."""
@@ -274,7 +314,8 @@ def main():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--gather-format", choices=("wire", "rows"), default="wire",
                     help="C5 (--gpus > 1, packed obs): what each step gathers to rank 0 -- st_step_wire's "
-                         "bit stream (28 B per 10x20 env) or st_step's obs/reward/done rows (48 B)")
+                         "bit stream (8 words = 32 B per 10x20 env: the obs bits, the reward's 32 bits, done; "
+                         "rank 0 decodes it inside the timed region) or st_step's obs/reward/done rows (48 B)")
     ap.add_argument("--rollout-chunk", type=int, default=100, help="steps per st_rollout launch")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -313,6 +354,14 @@ def main():
 
     from gym_simpletetris_amd import _lib as C
     from gym_simpletetris_amd.distributed import ShardedTetris, output_buffer, buffer_views
+
+    # which device every rank runs on, gathered over the process group (RCCL
+    # with the nccl backend), so the driver's N-GPU record shows that the
+    # collective formed an N-rank communicator over N distinct GPUs
+    topo = rank_topology(dev, rank, local_rank, world, use_dist, args.backend)
+    if use_dist and topo["distinct_devices"] != world and not shared:
+        raise SystemExit(f"bench: {world} ranks but {topo['distinct_devices']} distinct devices: "
+                         f"{topo['devices']} (set ST_BENCH_SHARED_GPU=1 only for tests that share one GPU)")
 
     W, H = 10, 20
     K, WU = args.steps, args.warmup
@@ -370,7 +419,7 @@ def main():
         summed on s after everything enqueued before the region and read
         after it (no blocking host read between the warm-up and the region:
         a thread that just slept in a long wait issues its next launches
-        slowly, tools/k20_idle.py / k20_sync.py)."""
+        slowly: round 4's k20_idle / k20_sync probes, in git history)."""
         with torch.cuda.stream(s):  # s is current for the whole region (graph replay launches on it)
             c0 = spawned_dev(eng, 0)
             ev0.record(s)  # first host calls after a stream switch are slow: not inside the region
@@ -827,6 +876,10 @@ def main():
         "p_lock": hm["p_lock"],
         "event_ms_per_step": hm["event_ms_per_step"],
         "roofline": hm["roofline"],
+        "ranks_seen": topo["ranks_seen"],
+        "distinct_devices": topo["distinct_devices"],
+        "rccl_version": topo["rccl_version"],
+        "topology": topo,
     }
     if "region_probe" in hm:
         out["debug"] = {"region_probe": hm["region_probe"]}
@@ -969,7 +1022,8 @@ def vec_env_variant(n: int, steps: int, dev):
     calls it: wall time per step, packed and float32 obs, without the action
     check, with the step kernel's own check ('async', the default: a sticky
     flag in mapped host memory, st_set_action_flag; no extra launch, no sync)
-    and with the per-step device->host check (True); copy=True (default)
+    and with the reference's immediate check (True: the action gate,
+    st_gate_actions, the host waiting for the check kernel only); copy=True (default)
     and, with 'async', copy=False, and copy=True with every step's outputs
     kept for 8 steps (`/held8`: no slot is free to reuse)."""
     from gym_simpletetris_amd.envs.tetris_env import TetrisVecEnv
@@ -1004,8 +1058,10 @@ def vec_env_variant(n: int, steps: int, dev):
                    "step's outputs in tensors of their own, never written again while the caller holds "
                    "any of them (a recent step's slot is reused once nothing of it is referenced: "
                    "slots_reused); copy=False: two alternating output slots (overwritten two steps "
-                   "later); held8: copy=True with each step's outputs kept 8 steps; host-bound above the "
-                   "kernel (DESIGN.md §5.1)")
+                   "later); held8: copy=True with each step's outputs kept 8 steps (the slot pool "
+                   "follows the holding depth: 9 slots, reused in turn); validate_actions=True: the "
+                   "action gate (st_gate_actions + the gated step, the host waiting for the check "
+                   "kernel only); host-bound above the kernel (DESIGN.md §5.1)")
     return out
 
 

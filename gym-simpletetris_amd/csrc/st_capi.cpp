@@ -24,6 +24,16 @@ struct st_ctx {
     uint32_t *mt;
     uint32_t *act_flag;  // st_set_action_flag (caller-owned), or null
     int cus;             // compute units of the device
+    // st_gate_actions / st_gate_wait: the gate word (device), its host copy
+    // (pinned, mapped), the event recorded behind the gate kernel, the last
+    // epoch, and whether the next step launch is gated / a wait is pending
+    uint32_t *gate;
+    uint32_t *gate_host;
+    uint32_t *gate_host_dev;
+    hipEvent_t gate_ev;
+    uint32_t gate_epoch;
+    bool gate_armed;
+    bool gate_pending;
 };
 
 namespace {
@@ -87,6 +97,11 @@ void free_state(st_ctx *c) {
     if (c->stats) (void)hipFree(c->stats);
     if (c->mt) (void)hipFree(c->mt);
     if (c->stamps) (void)hipFree(c->stamps);
+    if (c->gate) (void)hipFree(c->gate);
+    if (c->gate_host) (void)hipHostFree(c->gate_host);
+    if (c->gate_ev) (void)hipEventDestroy(c->gate_ev);
+    c->gate = c->gate_host = c->gate_host_dev = nullptr;
+    c->gate_ev = nullptr;
     c->stamps = nullptr;
     c->board = c->piece = c->mt = nullptr;
     c->stats = nullptr;
@@ -203,6 +218,11 @@ static int step_impl(st_ctx *c, const uint8_t *d_actions, uint32_t *d_obs, float
     p.done = d_done;
     p.final_obs = d_final_obs;
     p.info = d_info;
+    if (c->gate_armed) {  // st_gate_actions ran for this step: skip it all if it saw a bad action
+        p.gate = c->gate;
+        p.gate_epoch = c->gate_epoch;
+        c->gate_armed = false;
+    }
     ST_HIP(st::launch_step(p, (hipStream_t)stream));
     return ST_OK;
 }
@@ -478,6 +498,69 @@ int st_check_actions(const uint8_t *d_actions, int64_t n, uint32_t *d_flag, st_s
 int st_set_action_flag(st_ctx *c, uint32_t *d_flag) {
     if (!c) return fail(ST_EINVAL, "st_set_action_flag: null context");
     c->act_flag = d_flag;
+    return ST_OK;
+}
+
+int st_gate_actions(st_ctx *c, const uint8_t *d_actions, st_stream stream) {
+    if (!c || !d_actions) return fail(ST_EINVAL, "st_gate_actions: null argument");
+    DeviceGuard g(c->device);
+    if (!c->gate) {  // first use: the gate word, its mapped host copy, the event
+        ST_HIP(hipMalloc(&c->gate, sizeof(uint32_t)));
+        ST_HIP(hipMemset(c->gate, 0, sizeof(uint32_t)));
+        ST_HIP(hipHostMalloc(&c->gate_host, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
+        *c->gate_host = 0;
+        void *dp = nullptr;
+        ST_HIP(hipHostGetDevicePointer(&dp, c->gate_host, 0));
+        c->gate_host_dev = static_cast<uint32_t *>(dp);
+        ST_HIP(hipEventCreateWithFlags(&c->gate_ev, hipEventDisableTiming));
+    }
+    c->gate_epoch = c->gate_epoch + 1u ? c->gate_epoch + 1u : 1u;  // never 0 (the words' initial value)
+    hipStream_t s = (hipStream_t)stream;
+    ST_HIP(st::launch_gate_actions(d_actions, c->n, c->gate, c->gate_host_dev, c->gate_epoch, s));
+    ST_HIP(hipEventRecord(c->gate_ev, s));
+    c->gate_armed = true;
+    c->gate_pending = true;
+    return ST_OK;
+}
+
+int st_gate_wait(st_ctx *c) {
+    if (!c) return fail(ST_EINVAL, "st_gate_wait: null context");
+    if (!c->gate_pending) return fail(ST_ESTATE, "st_gate_wait without st_gate_actions");
+    c->gate_pending = false;
+    DeviceGuard g(c->device);
+    ST_HIP(hipEventSynchronize(c->gate_ev));
+    return __atomic_load_n(c->gate_host, __ATOMIC_ACQUIRE) == c->gate_epoch ? 1 : 0;
+}
+
+int st_stream_wait(st_stream waiter, st_stream signaller) {
+    if (waiter == signaller) return ST_OK;
+    int dev = 0;
+    ST_HIP(hipGetDevice(&dev));
+    // one reusable event per (device, signalling stream) and thread: a wait
+    // enqueued by hipStreamWaitEvent keeps the record it saw, so re-recording
+    // the event for the next call is safe
+    struct Ev {
+        int dev;
+        st_stream s;
+        hipEvent_t ev;
+    };
+    thread_local Ev cache[16];
+    thread_local int used = 0;
+    hipEvent_t ev = nullptr;
+    for (int i = 0; i < used; ++i)
+        if (cache[i].dev == dev && cache[i].s == signaller) ev = cache[i].ev;
+    if (!ev) {
+        ST_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        if (used < 16) {
+            cache[used++] = Ev{dev, signaller, ev};
+        } else {  // evict the oldest entry
+            (void)hipEventDestroy(cache[0].ev);
+            for (int i = 1; i < 16; ++i) cache[i - 1] = cache[i];
+            cache[15] = Ev{dev, signaller, ev};
+        }
+    }
+    ST_HIP(hipEventRecord(ev, (hipStream_t)signaller));
+    ST_HIP(hipStreamWaitEvent((hipStream_t)waiter, ev, 0));
     return ST_OK;
 }
 

@@ -41,7 +41,10 @@ struct KParams {
                         // stores dropped, 8192 = late counter loads from the
                         // first workgroup's lines, 16384 / 32768 = the logic /
                         // draw wave's part of 2048 only; 65536 / 131072 = the
-                        // draw wave's count / MT-word store only
+                        // draw wave's count / MT-word store only; 262144 = the draw
+                        // wave's count rows T J L Z not loaded, 524288 = MT windows
+                        // read as zeros, 1048576 = no next-generation chunks,
+                        // 2097152 = the lock-path counter rows not loaded
     uint64_t *stamps;   // DIAGNOSTIC build only (env ST_STAMPS at st_create): per-wave
                         // s_memtime at 8 phase boundaries of the step kernel
     int32_t k;          // st_rollout: number of steps
@@ -65,6 +68,12 @@ struct KParams {
     uint32_t *wire;          // st_step_wire: [st_wire_words(W, H)][n] gather format, or null
     int32_t *info;           // st_step_vec: [ST_NSTAT][n] counters after the step, or null
     int32_t cus;             // compute units of the device (launch_rollout's kernel choice)
+    // st_gate_actions: the step skips every env (no state change, no output)
+    // when *gate == gate_epoch, i.e. the gate check before it saw an action
+    // outside 0..6 (the reference's KeyError before any state change,
+    // tetris_env.py:245); null: no gate (every launch but a gated one)
+    const uint32_t *gate;
+    uint32_t gate_epoch;
 };
 
 hipError_t launch_seed(const KParams &p, hipStream_t s);
@@ -83,6 +92,8 @@ hipError_t launch_grayscale(const KParams &p, const uint32_t *obs, int size, int
 hipError_t launch_unwire(int W, int H, int64_t n_global, int shards, int64_t n_cap, const uint32_t *wire,
                          uint32_t *obs, int32_t *reward, uint8_t *done, hipStream_t s);
 hipError_t launch_check_actions(const uint8_t *a, int64_t n, uint32_t *flag, hipStream_t s);
+hipError_t launch_gate_actions(const uint8_t *a, int64_t n, uint32_t *gate, uint32_t *host_flag, uint32_t epoch,
+                               hipStream_t s);
 hipError_t launch_gen_actions(uint8_t *out, int64_t n, int64_t t, uint64_t seed, int64_t off,
                               hipStream_t s);
 

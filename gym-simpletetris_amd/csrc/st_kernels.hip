@@ -1137,7 +1137,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                                                 (qbase(q) + 4 <= kHotRows ? loff : clamp_off(q, kHotRows)));
     };
     if (mine_q(0)) sv0 = ldq(0);
-    if (mine_q(1)) sv1 = ldq(1);
+    // (ablation 262144: st_step's draw wave does not load shape counts T J L Z -- timing only)
+    if (mine_q(1) && !(LCL && (kAblate & 262144u))) sv1 = ldq(1);
     if (mine_q(2)) sv2 = ldq(2);
     if (mine_q(3)) sv3 = ldq(3);
     const int K = KSTEPS ? KSTEPS : p.k;
@@ -1150,6 +1151,12 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     // unconditional (clamped) so it is issued with the others; masked at use
     uint32_t act_next = 0;
     if constexpr (ACT) act_next = p.actions[real ? e : p.n - 1];
+    // st_gate_actions (VEC instantiations, which every gated launch uses):
+    // the gate word, loaded with the prologue's burst (an empty range reads 0
+    // when the launch is not gated), tested after B0 -- before any global
+    // store of either wave
+    [[maybe_unused]] uint32_t gate_v = 0;
+    if constexpr (VEC) gate_v = __builtin_amdgcn_raw_buffer_load_b32(buf_rsrc(p.gate, 4u), 0u, 0, 0);
     // two-wave st_step: the logic wave also fetches its piece word and clock
     // per env (4 B/lane from lines the state loads fetch anyway), so the
     // action phase starts from registers instead of an LDS read after B0
@@ -1231,6 +1238,11 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     if (ROLE == kRoleL && lane == 0) sm.f1 = 0u;
     if (ROLE == kRoleD && lane == 0) sm.f2 = 0u;
     wg_barrier();  // B0: the staged state is complete
+    if constexpr (VEC) {
+        // a gate that saw an action outside 0..6: no env steps (both waves
+        // leave here, before B1 and before any global store)
+        if (p.gate && __builtin_amdgcn_readfirstlane(gate_v) == p.gate_epoch) return;
+    }
     auto ss = [&](int r) -> uint32_t & { return SS[r * kWave + lane]; };
     auto tab = [&](int i) -> uint2 { return *reinterpret_cast<const uint2 *>(&sm.T2[2 * i]); };
     // an action outside value_action_map in any step of this launch (the
@@ -1318,9 +1330,9 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         // (ablation 8192: from the first workgroup's lines -- their HBM reads gone, timing only)
         const uint32_t eo = (kAblate & 8192u) ? (uint32_t)lane * 4u : (uint32_t)e * 4u;
 #pragma unroll
-        for (int j = 0; j < 5; ++j)
+        for (int j = 0; j < 5; ++j)  // (ablation 2097152: not loaded, timing only)
             lcv[j] = __builtin_amdgcn_raw_buffer_load_b32(
-                rs, locknow ? eo + (uint32_t)(ST_STAT_SCORE + j) * (uint32_t)sd * 4u : kOff,
+                rs, locknow && !(kAblate & 2097152u) ? eo + (uint32_t)(ST_STAT_SCORE + j) * (uint32_t)sd * 4u : kOff,
                 0, 0);
     }
     // the draw wave's next-generation chunk of this step: operands issued
@@ -1336,7 +1348,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     [[maybe_unused]] int32_t csid = 0;  // the spawned shape's count after the spawn
     if constexpr (DO_D) {
         mrs = mt_res(p.mt + e0 * kMtPitch, lane);
-        mt_chunk_issue(mrs, mt0, real && !(kAblate & 2u), lane, chunk);
+        mt_chunk_issue(mrs, mt0, real && !(kAblate & (2u | 1048576u)), lane, chunk);  // (1048576: no chunks, timing only)
         const int s0 = pv_id(mt0);
 #pragma unroll
         for (int i = 0; i < 7; ++i) cnt[i] = (int32_t)ss(ST_STAT_COUNT0 + i) + (i == s0);  // _new_piece :199
@@ -1345,8 +1357,10 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         for (int i = 1; i < 7; ++i) csid = s0 == i ? cnt[i] : csid;
         dpar = draw_par(cnt);
     }
+    [[maybe_unused]] uint64_t lockball = 0;  // the wave's locking lanes
     if constexpr (DO_L) {
         const uint64_t m = __ballot(locknow);
+        lockball = m;
         if (lane == 0) {
             sm.lockm[t & 1][0] = (uint32_t)m;
             sm.lockm[t & 1][1] = (uint32_t)(m >> 32);
@@ -1371,7 +1385,71 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     const bool want_pre = locknow && !(kAblate & 2u);
     constexpr int kWin = STEP2 ? 8 : 16;
     MtPre pre;
-    if constexpr (DO_D) mt_pre_load<kWin>(mrs, mtst, want_pre, pre);
+    // (ablation 524288: the window's words read as zeros, no traffic -- timing only)
+    if constexpr (DO_D) mt_pre_load<kWin>(mrs, mtst, want_pre && !(kAblate & 524288u), pre);
+
+    // ---------------- st_step: early stores (round 6) ----------------
+    // Everything a lane that does not lock outputs is final once its action
+    // phase is done: reward (reward_step's 1 or 0, :256), done = 0, the clock,
+    // the piece word, and its obs -- the unchanged board with the piece at
+    // its new position (:301-302).  Those stores go out here, before the lock
+    // path, instead of in the grid-wide store burst after it: the memory
+    // system is idle while the waves run their lock paths.  The obs rows go
+    // as 16-B groups of 4 envs, so a group holding a locking env waits for
+    // the late pass.  EARLY = 0 keeps the round-5 schedule (A/B builds).
+#ifndef ST_EARLY
+#define ST_EARLY 0
+#endif
+    constexpr bool EARLY = ST_EARLY && KSTEPS == 1 && !VEC && DO_L;
+    [[maybe_unused]] const bool wide_obs1 = OVP && (p.n & 3) == 0 && e0 + kWave <= p.n &&
+                                            (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0 &&
+                                            (!VEC || (reinterpret_cast<uintptr_t>(p.final_obs) & 15u) == 0);
+    // this lane's 4-env group (envs 4 (lane % 16) .. + 3) holds a locking env
+    [[maybe_unused]] const bool grp_lock = ((lockball >> (4 * (lane & 15))) & 0xFull) != 0;
+    if constexpr (EARLY) {
+        // the overlay of the non-locking lanes (the current piece); locking
+        // lanes write a dump slot (an address select, no branch)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t *dst = &sm.OV[(ax + pc_dx(desc.y, j) + kPad) * kWave + lane];
+            *(locknow ? &sm.dump[lane] : dst) = pc_bits<S32>(desc.x, j, ay) & hmask;
+        }
+        const auto rr = buf_rsrc(p.reward, (uint32_t)p.n * 4u);
+        const auto rd = buf_rsrc(p.done, (uint32_t)p.n);
+        const bool now = real && !locknow;
+        __builtin_amdgcn_raw_buffer_store_b32(rew, rr, now ? (uint32_t)e * 4u : kOff, 0, kRD);
+        __builtin_amdgcn_raw_buffer_store_b8((char)0, rd, now ? (uint32_t)e : kOff, 0, kRD);
+        {
+            const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
+            const uint32_t eo = (uint32_t)e * 4u;
+            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)time, rs,
+                                                  !locknow ? eo + (uint32_t)ST_STAT_TIME * (uint32_t)sd * 4u : kOff, 0, kST);
+            __builtin_amdgcn_raw_buffer_store_b32(pack_piece(id, rot, ax, ay, lock), rs,
+                                                  !locknow ? eo + (uint32_t)kPieceRow * (uint32_t)sd * 4u : kOff, 0, kST);
+        }
+        wave_sync();
+        uint4 bw[NBQ], ow[NBQ];
+#pragma unroll
+        for (int q = 0; q < NBQ; ++q) {
+            if (WT || 4 * q < W) {
+                bw[q] = *reinterpret_cast<const uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]);
+                ow[q] = *reinterpret_cast<const uint4 *>(&sm.OV[(4 * q + lrow + kPad) * kWave + lcc]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const auto ro = buf_rsrc(wide_obs1 ? p.obs : nullptr, (uint32_t)W * (uint32_t)p.n * 4u);
+#pragma unroll
+        for (int q = 0; q < NBQ; ++q) {
+            if (WT || 4 * q < W) {
+                const uint4 v = bw[q], o = ow[q];
+                const uint4 ob = make_uint4((v.x | o.x) & hmask, (v.y | o.y) & hmask, (v.z | o.z) & hmask,
+                                            (v.w | o.w) & hmask);
+                const uint32_t ooff = ((uint32_t)e0 + (uint32_t)(4 * q + lrow) * (uint32_t)p.n + (uint32_t)lcc) * 4u;
+                buf_store16<kNT>(ro, grp_lock ? kOff : ooff, ob);
+            }
+        }
+        ST_STAMP(9);  // (logic wave: the early stores issued)
+    }
 
     // ---------------- logic: lock path (tetris_env.py:263-299) ----------------
     bool died = false, spawn = false;
@@ -1530,8 +1608,9 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         // skipped on some path would make a later load's wait vmcnt(0).
         const auto rr = buf_rsrc(p.reward ? p.reward + (int64_t)t * p.n : nullptr, (uint32_t)p.n * 4u);
         const auto rd = buf_rsrc(p.done ? p.done + (int64_t)t * p.n : nullptr, (uint32_t)p.n);
-        __builtin_amdgcn_raw_buffer_store_b32(rew, rr, real ? (uint32_t)e * 4u : kOff, 0, kRD);
-        __builtin_amdgcn_raw_buffer_store_b8((char)(died ? 1 : 0), rd, real ? (uint32_t)e : kOff, 0, kRD);
+        const bool late = real && (!EARLY || locknow);  // EARLY: the other lanes stored theirs already
+        __builtin_amdgcn_raw_buffer_store_b32(rew, rr, late ? (uint32_t)e * 4u : kOff, 0, kRD);
+        __builtin_amdgcn_raw_buffer_store_b8((char)(died ? 1 : 0), rd, late ? (uint32_t)e : kOff, 0, kRD);
     }
     if constexpr (DO_L && KSTEPS == 1) {
         // The post-step board never depends on the spawned piece either (a
@@ -1560,8 +1639,12 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             const uint32_t om = spawn ? pd.x : desc.x, og = spawn ? pd.y : desc.y;
             const int ox = spawn ? W / 2 : ax, oy = spawn ? 0 : ay;
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                sm.OV[(ox + pc_dx(og, j) + kPad) * kWave + lane] = pc_bits<S32>(om, j, oy) & hmask;
+            for (int j = 0; j < 4; ++j) {
+                // (EARLY: the non-locking lanes painted theirs before the lock path)
+                uint32_t *dst = &sm.OV[(ox + pc_dx(og, j) + kPad) * kWave + lane];
+                if constexpr (EARLY) dst = locknow ? dst : &sm.dump[lane];
+                *dst = pc_bits<S32>(om, j, oy) & hmask;
+            }
         }
         sm.KM[lane] = reset_now ? 0u : hmask;
         sm.BD[lane] = bdirty;
@@ -1588,9 +1671,6 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         // the board array as one resource: byte offsets < W * stride * 4 <= 2^31
         const auto rb = buf_rsrc(p.board, (uint32_t)W * (uint32_t)sd * 4u);
         const uint32_t boff = ((uint32_t)e0 * 4u + loff * 4u);
-        const bool wide_obs1 = OVP && (p.n & 3) == 0 && e0 + kWave <= p.n &&
-                               (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0 &&
-                               (!VEC || (reinterpret_cast<uintptr_t>(p.final_obs) & 15u) == 0);
         // obs rows board | overlay (a reset env's terminal board included):
         // no branch around the stores (a store on one path only made the
         // compiler wait for every LDS read at the join) -- a null range
@@ -1617,7 +1697,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                         const uint4 keep = p.final_obs ? km : make_uint4(~0u, ~0u, ~0u, ~0u);
                         buf_store16<kNT>(ro, ooff, make_uint4(ob.x & keep.x, ob.y & keep.y, ob.z & keep.z, ob.w & keep.w));
                     } else {
-                        buf_store16<kNT>(ro, ooff, ob);
+                        // (EARLY: groups without a locking env went out before the lock path)
+                        buf_store16<kNT>(ro, EARLY && !grp_lock ? kOff : ooff, ob);
                     }
                 }
                 v.x &= km.x;
@@ -1793,8 +1874,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, on ? eo + (uint32_t)r * (uint32_t)sd * 4u : kOff,
                                                       0, kST);
             };
-            put(ST_STAT_TIME, time, true);
-            put(kPieceRow, (int32_t)pw_out, true);
+            put(ST_STAT_TIME, time, !EARLY || locknow);  // (EARLY: the others went out before the lock path)
+            put(kPieceRow, (int32_t)pw_out, !EARLY || locknow);
             const bool cst = !(kAblate & (2048u | 16384u));  // (ablation: lock-path counter stores dropped)
             put(ST_STAT_SCORE, score, cst && locknow && score != o_score);
             put(ST_STAT_LINES, lines, cst && locknow && lines != o_lines);
@@ -3677,6 +3758,29 @@ __global__ __launch_bounds__(256) void k_check_actions(const uint8_t *__restrict
     if (bad) flag[0] = 1u;
 }
 
+// st_gate_actions: the same test, writing the call's epoch (never 0) to the
+// context's gate word and to the caller-visible host word where any action
+// is outside 0..6.  Every writer stores the same value, so plain stores
+// suffice, and the words need no reset between calls: a gated step compares
+// the gate with its own epoch (KParams::gate_epoch).
+__global__ __launch_bounds__(256) void k_gate_actions(const uint8_t *__restrict__ a, int64_t n, uint32_t *gate,
+                                                      uint32_t *host_flag, uint32_t epoch) {
+    const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+    if (i0 >= n) return;
+    bool bad = false;
+    if (i0 + 16 <= n && (reinterpret_cast<uintptr_t>(a + i0) & 15u) == 0) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(a + i0);
+        auto over6 = [](uint32_t w) { return ((((w & 0x7F7F7F7Fu) + 0x79797979u) | w) & 0x80808080u) != 0u; };
+        bad = over6(v.x) || over6(v.y) || over6(v.z) || over6(v.w);
+    } else {
+        for (int64_t i = i0; i < n && i < i0 + 16; ++i) bad = bad || a[i] > 6;
+    }
+    if (bad) {
+        gate[0] = epoch;
+        host_flag[0] = epoch;
+    }
+}
+
 // ---------------------------------------------------------------- greedy policy
 // Benchmark / test workload generator (not part of the reference env): the
 // action a greedy placement player takes in every env's current state, so
@@ -3779,7 +3883,7 @@ hipError_t launch_step(const KParams &p, hipStream_t s) {
     const dim3 grid((unsigned)(p.stride / kWave)), block(2 * kWave);  // logic + draw wave
     const bool f32 = p.obs_f32 != nullptr;
     const bool sc0 = !(p.flags & kScoringFlags);
-    if (p.final_obs || p.info) {  // st_step_vec: the vector env's outputs (VEC)
+    if (p.final_obs || p.info || p.gate) {  // st_step_vec: the vector env's outputs (VEC); gated launches
         if (p.W == 10 && p.H == 20) {
             if (f32 && sc0) hipLaunchKernelGGL((k_step<10, 20, true, false, true, true>), grid, block, 0, s, ST_STEP_ARGS(p));
             else if (f32) hipLaunchKernelGGL((k_step<10, 20, true, false, false, true>), grid, block, 0, s, ST_STEP_ARGS(p));
@@ -3957,6 +4061,14 @@ hipError_t launch_check_actions(const uint8_t *a, int64_t n, uint32_t *flag, hip
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_check_actions, dim3((unsigned)((n + 16 * 256 - 1) / (16 * 256))), dim3(256), 0, s, a,
                        n, flag);
+    return hipGetLastError();
+}
+
+hipError_t launch_gate_actions(const uint8_t *a, int64_t n, uint32_t *gate, uint32_t *host_flag, uint32_t epoch,
+                               hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gate_actions, dim3((unsigned)((n + 16 * 256 - 1) / (16 * 256))), dim3(256), 0, s, a, n,
+                       gate, host_flag, epoch);
     return hipGetLastError();
 }
 

@@ -10,11 +10,14 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# ST_LIB overrides the library path (diagnostic A/B builds only).
+# ST_LIB overrides the library path (a custom or variant build).  A build of
+# another ABI version is refused unless ST_AB_OLD_ABI=1 (diagnostic A/Bs of
+# older builds only: then missing entry points are tolerated and st_state is
+# disabled, with a warning).
 LIB_PATH = os.environ.get("ST_LIB") or os.path.join(_HERE, "libsimpletetris.so")
 
 ST_OK, ST_EINVAL, ST_ENOMEM, ST_EHIP, ST_ESTATE = 0, -1, -2, -3, -4
-ABI_VERSION = 2  # ST_ABI_VERSION of include/simpletetris.h
+ABI_VERSION = 3  # ST_ABI_VERSION of include/simpletetris.h
 
 # st_flags (include/simpletetris.h) keyed by the reference kwarg names
 # (TetrisEngine.__init__, tetris_env.py:126-137).
@@ -40,8 +43,8 @@ EXPORT_MT, EXPORT_OBS_F32 = 1, 2  # st_export_env parts
 EXPORTS = ("st_create", "st_destroy", "st_seed", "st_reset", "st_step", "st_step_f32", "st_step_vec", "st_rollout",
            "st_wire_words", "st_step_wire", "st_unwire", "st_unwire_shards",
            "st_obs_to_f32", "st_render", "st_grayscale", "st_state", "st_copy", "st_mt_sync", "st_state_bytes", "st_save",
-           "st_load", "st_export_env", "st_export_words", "st_check_actions", "st_set_action_flag", "st_stream_sync",
-           "st_host_device_ptr", "st_gen_actions", "st_policy_greedy", "st_debug_stamps", "st_last_error", "st_abi_version")
+           "st_load", "st_export_env", "st_export_words", "st_check_actions", "st_set_action_flag", "st_gate_actions",
+           "st_gate_wait", "st_stream_sync", "st_host_device_ptr", "st_stream_wait", "st_gen_actions", "st_policy_greedy", "st_debug_stamps", "st_last_error", "st_abi_version")
 
 
 class StError(RuntimeError):
@@ -107,24 +110,36 @@ def load(path: str = LIB_PATH):
         "st_export_words": ([i32, i32], ctypes.c_int),
         "st_check_actions": ([vp, i64, vp, vp], ctypes.c_int),
         "st_set_action_flag": ([vp, vp], ctypes.c_int),
+        "st_gate_actions": ([vp, vp, vp], ctypes.c_int),
+        "st_gate_wait": ([vp], ctypes.c_int),
         "st_stream_sync": ([vp], ctypes.c_int),
         "st_host_device_ptr": ([vp, ctypes.POINTER(vp)], ctypes.c_int),
+        "st_stream_wait": ([vp, vp], ctypes.c_int),
         "st_gen_actions": ([vp, i64, i64, u64, i64, vp], ctypes.c_int),
         "st_policy_greedy": ([vp, u64, i64, ctypes.c_uint32, vp, vp], ctypes.c_int),
         "st_debug_stamps": ([vp, vp, i64], ctypes.c_int),
         "st_last_error": ([], ctypes.c_char_p),
         "st_abi_version": ([], ctypes.c_int),
     }
-    ab_override = "ST_LIB" in os.environ  # diagnostic A/B of older builds: tolerate
-    for name, (args, res) in sig.items():  # entry points they predate
+    # ST_AB_OLD_ABI=1: a diagnostic A/B of an older build -- tolerate the
+    # entry points it predates (never the default, not even with ST_LIB set)
+    ab_override = os.environ.get("ST_AB_OLD_ABI") == "1"
+    L.st_abi_version.argtypes = []
+    L.st_abi_version.restype = ctypes.c_int
+    abi = L.st_abi_version()
+    if abi != ABI_VERSION and not ab_override:
+        raise ImportError(f"{path}: libsimpletetris ABI {abi} != {ABI_VERSION} (rebuild it, or set "
+                          "ST_AB_OLD_ABI=1 for a diagnostic A/B of an older build)")
+    for name, (args, res) in sig.items():
         if ab_override and not hasattr(L, name):
             continue
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
-    if L.st_abi_version() != ABI_VERSION:
-        if not ab_override:
-            raise ImportError(f"libsimpletetris ABI {L.st_abi_version()} != {ABI_VERSION}")
+    if abi != ABI_VERSION:
+        import warnings
+        warnings.warn(f"ST_AB_OLD_ABI=1: {path} has ABI {abi}, this package {ABI_VERSION}; "
+                      "st_state disabled (raw ctypes A/Bs only)")
         # the state-view struct may differ across ABIs: an older build
         # serves raw ctypes A/Bs only (views read through the wrong struct
         # size tensors from garbage)

@@ -206,13 +206,18 @@ class TetrisBatch:
             raise ValueError(f"{name} must have {self.n} entries, got {t.numel()}")
         return t.contiguous()
 
-    def _actions(self, x, lead=()) -> torch.Tensor:
+    def _actions(self, x, lead=(), gate: bool = False):
         """Actions as a contiguous uint8 device tensor of shape lead + (n,).
         The reference raises KeyError for an action outside value_action_map
         (tetris_env.py:152-160, :245); a uint8 cast would wrap -1 to 255 and
         263 to 7, so values are checked BEFORE it:
-          validate_actions=True: on the host, immediately (for a device tensor
-            one device->host sync);
+          validate_actions=True: immediately.  Host arrays on the host; a
+            device tensor, with `gate` (step() / the vector env's step): by
+            st_gate_actions -- returned as (tensor, True), and the caller
+            gates its step launch on it and calls _gate_wait() after it (the
+            step is skipped entirely if an action was bad; the host waits for
+            the check kernel only, not the stream); without `gate`
+            (rollouts, step_wire) one device->host sync;
           'async': by the step kernel itself (st_set_action_flag: the kernel
             sets a sticky word in mapped host memory when an action is > 6,
             polled here without a sync); non-uint8 tensors get their bad values
@@ -220,31 +225,39 @@ class TetrisBatch:
           False: no check (values > 6 act as idle)."""
         shape = tuple(lead) + (self.n,)
         asyn = self.validate_actions == "async"
+        gated = gate and self.validate_actions is True
         if asyn:
             self._raise_flagged()
-        if (self.validate_actions is not True and type(x) is torch.Tensor and x.dtype == torch.uint8
-                and x.device == self.device and x.is_contiguous() and tuple(x.shape) == shape):
-            return x  # an RL loop's own device buffer: checked in the step kernel ('async') or not at all
+        if (type(x) is torch.Tensor and x.dtype == torch.uint8 and x.device == self.device
+                and x.is_contiguous() and tuple(x.shape) == shape):
+            # an RL loop's own device buffer: checked in the step kernel
+            # ('async'), by the gate (True), or not at all
+            if gated:
+                return x, True
+            if self.validate_actions is not True:
+                return (x, False) if gate else x
         x = _from_dlpack(x)
         if isinstance(x, torch.Tensor):
             if x.is_complex():
                 raise TypeError(f"actions must be real numbers, got {x.dtype}")
             if tuple(x.shape) != shape and x.numel() != int(np.prod(shape)):
                 raise ValueError(f"actions must have shape {shape}, got {tuple(x.shape)}")
-            if self.validate_actions is True or x.device != self.device:
+            on_dev = x.device == self.device
+            if (self.validate_actions is True and not (gated and on_dev)) or not on_dev:
                 bad = _bad_actions(x)
                 if bool(bad.any()):
                     v = x[bad].flatten()[0].item()
                     raise KeyError(f"action {v} not in 0..6 (tetris_env.py:245)")
-            if x.dtype == torch.uint8 and x.device == self.device:
+            if x.dtype == torch.uint8 and on_dev:
                 t = x
             else:
                 t = x.to(device=self.device).to(torch.uint8)
-                if asyn:  # keep bad values visible to the kernel's check: a cast may wrap them
-                    # into 0..6 (int16 256 -> 0, 2.5 -> 2); the sentinel is set after the cast,
-                    # in uint8, so no source dtype has to hold 255 (int8 cannot)
+                if asyn or (gated and on_dev):  # keep bad values visible to the kernel's check: a cast
+                    # may wrap them into 0..6 (int16 256 -> 0, 2.5 -> 2); the sentinel is set after
+                    # the cast, in uint8, so no source dtype has to hold 255 (int8 cannot)
                     t = t.masked_fill_(_bad_actions(x).to(self.device), 255)
-            return t.reshape(shape).contiguous()
+            t = t.reshape(shape).contiguous()
+            return (t, gated and on_dev) if gate else t
         a = np.asarray(x)
         if a.size != int(np.prod(shape)):
             raise ValueError(f"actions must have shape {shape}, got {a.shape}")
@@ -257,7 +270,23 @@ class TetrisBatch:
         if a.size and not ok.all():
             v = a.flat[np.flatnonzero(~ok)[0]]
             raise KeyError(f"action {v} not in 0..6 (tetris_env.py:245)")
-        return torch.as_tensor(a.astype(np.uint8).reshape(shape), device=self.device)
+        t = torch.as_tensor(a.astype(np.uint8).reshape(shape), device=self.device)
+        return (t, False) if gate else t
+
+    def _gate_launch(self, a: torch.Tensor, s) -> None:
+        """st_gate_actions: check `a` on stream s; the next step launch on
+        this context is skipped if an action is outside 0..6."""
+        C.check(self._L.st_gate_actions(self._ctx, _ptr(a), s))
+
+    def _gate_wait(self) -> None:
+        """st_gate_wait: wait for the gate's check (not the step behind it)
+        and raise the reference's KeyError (tetris_env.py:245) if it saw an
+        action outside 0..6 -- the gated step changed nothing."""
+        rc = self._L.st_gate_wait(self._ctx)
+        if rc < 0:
+            C.check(rc)
+        if rc:
+            raise KeyError("an action outside 0..6 (tetris_env.py:245); no env was stepped")
 
     def _raise_flagged(self):
         if self._flag_np[0]:
@@ -289,7 +318,7 @@ class TetrisBatch:
         done uint8/bool [n]) device tensors (e.g. a gather buffer's views)."""
         if obs not in ("packed", "f32", "none"):
             raise ValueError("obs must be 'packed', 'f32' or 'none'")
-        a = self._actions(actions)
+        a, gated = self._actions(actions, gate=True)
         o_t, r_t, d_t = (self.obs, self.reward, self.done) if out is None else out
         if out is not None:
             for t, dt, shape in ((o_t, torch.int32, (self.width, self.n)),
@@ -300,6 +329,8 @@ class TetrisBatch:
                     raise ValueError(f"out tensor {tuple(t.shape)} {t.dtype} on {t.device}: "
                                      f"need contiguous {shape} on {self.device}")
         s = self._stream()
+        if gated:  # validate_actions=True, device actions: the gated step (st_gate_actions)
+            self._gate_launch(a, s)
         # no torch.cuda.device() context: st_step selects the context's device itself
         if obs == "f32":
             if self.obs_f32 is None:
@@ -307,9 +338,13 @@ class TetrisBatch:
                                            dtype=torch.float32, device=self.device)
             C.check(self._L.st_step_f32(self._ctx, _ptr(a), _ptr(o_t), _ptr(self.obs_f32),
                                         _ptr(r_t), _ptr(d_t), s))
+            if gated:
+                self._gate_wait()
             return self.obs_f32, r_t, d_t
         C.check(self._L.st_step(self._ctx, _ptr(a), _ptr(o_t) if obs == "packed" else None,
                                 _ptr(r_t), _ptr(d_t), s))
+        if gated:
+            self._gate_wait()
         return (o_t if obs == "packed" else None), r_t, d_t
 
     @property
@@ -553,6 +588,18 @@ def unwire_shards(recv: torch.Tensor, width: int, height: int, n_global: int, ou
         out = (torch.empty((width, n_global), dtype=torch.int32, device=recv.device),
                torch.empty(n_global, dtype=torch.int32, device=recv.device),
                torch.empty(n_global, dtype=torch.bool, device=recv.device))
+    else:  # the kernel writes through raw pointers: check every output like recv
+        out = tuple(out)
+        want = (((width, n_global), (torch.int32,)), ((n_global,), (torch.int32,)),
+                ((n_global,), (torch.bool, torch.uint8)))
+        if len(out) != 3:
+            raise ValueError("out must be (obs, reward, done)")
+        for name, t, (shape, dts) in zip(("obs", "reward", "done"), out, want):
+            if not isinstance(t, torch.Tensor) or t.device != recv.device or tuple(t.shape) != shape \
+                    or t.dtype not in dts or not t.is_contiguous():
+                got = (tuple(t.shape), t.dtype, t.device) if isinstance(t, torch.Tensor) else type(t)
+                raise ValueError(f"out {name}: need a contiguous {'/'.join(map(str, dts))} {shape} tensor "
+                                 f"on {recv.device}, got {got}")
     obs, reward, done = out
     with torch.cuda.device(recv.device):
         C.check(L.st_unwire_shards(width, height, n_global, shards, cap, _ptr(recv), _ptr(obs), _ptr(reward),

@@ -18,6 +18,7 @@ CPU fallback.
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import random
 import sys
@@ -97,6 +98,12 @@ class TetrisEnv:
         self.window = None
         self.clock = None
         self._stats = None         # last downloaded counters (host int64 [NSTAT])
+        # info['statistics'] is ONE dict for the env's lifetime, updated in
+        # place, like the reference's live shape_counts (tetris_env.py:181,
+        # :199, :240): a held info sees later spawns, and counts written into
+        # it weight the next draws (:183-191)
+        self._shape_counts = None
+        self._shape_vals = None    # what the env last wrote into it
         self._started = False
         self._rng_sync_state = None
         dev = self.engine.device
@@ -215,17 +222,56 @@ class TetrisEnv:
         return obs, int(rec[W]), bool(rec[W + 1]), st, img
 
     # ------------------------------------------------------------- gym API
-    @staticmethod
-    def _get_info(st):
+    def _get_info(self, st):
         """TetrisEngine.get_info (tetris_env.py:232-241); `st` holds Python
-        ints (the record's counter rows, .tolist())."""
+        ints (the record's counter rows, .tolist()).  'statistics' is the
+        env's one shape-count dict, refreshed in place (the reference returns
+        its live shape_counts, :240)."""
+        vals = tuple(st[_C0:_C0 + 7])
+        d = self._shape_counts
+        if d is None:
+            d = self._shape_counts = dict(zip(SHAPE_NAMES, vals))
+        elif vals != self._shape_vals:
+            for k, v in zip(SHAPE_NAMES, vals):
+                d[k] = v
+        self._shape_vals = vals
         return {"time": st[_TIME],
                 "current_piece": SHAPE_NAMES[st[_PIECE] & 7],
                 "score": st[_SCORE],
                 "lines_cleared": st[_LINES],
                 "holes": st[_HOLES],
                 "deaths": st[_DEATHS],
-                "statistics": dict(zip(SHAPE_NAMES, st[_C0:_C0 + 7]))}
+                "statistics": d}
+
+    def _push_counts(self):
+        """Counts the caller wrote into info['statistics'] since the last call
+        take effect like writes into the reference's shape_counts: the next
+        draw (:183-191) sees them, and spawns count on from them (:199).  The
+        device drops its preview (st_mt_sync: the piece drawn one spawn ahead
+        with the old counts) and takes the new counts."""
+        d = self._shape_counts
+        if d is None:
+            return
+        if len(d) == 7 and all(type(d.get(k)) is int for k in SHAPE_NAMES):
+            vals = tuple(d[k] for k in SHAPE_NAMES)
+            if vals == self._shape_vals:
+                return
+        else:
+            vals = None
+        if vals is None or not all(-(1 << 31) <= v < (1 << 31) for v in vals):
+            raise ValueError("info['statistics'] may only hold int32 counts for the keys "
+                             f"{SHAPE_NAMES} (got {dict(d)!r})")
+        eng = self.engine
+        L, s, v = eng._L, self._stream(), eng._views
+        C.check(L.st_mt_sync(eng._ctx, s))
+        cnt = np.asarray(vals, dtype=np.int32)
+        for i in range(7):
+            C.check(L.st_copy(ctypes.c_void_p(v.stats + (C.STAT["count0"] + i) * v.stride * 4),
+                              ctypes.c_void_p(cnt.ctypes.data + 4 * i), 4, s))
+        self._sync()  # (cnt is pageable host memory)
+        self._shape_vals = vals
+        if self._stats is not None:
+            self._stats[_C0:_C0 + 7] = list(vals)  # the reward-type test compares with these
 
     def _observation(self, obs, img):
         """TetrisEnv._observation (tetris_env.py:413-433) + float32 cast, from
@@ -255,6 +301,7 @@ class TetrisEnv:
         if not self._started:
             raise AttributeError("step() before reset(): the reference fails at tetris_env.py:244")
         action = scalar_action(action)  # value_action_map[action]'s KeyError, tetris_env.py:245
+        self._push_counts()
         prev = self._stats
         self._push_rng()
         eng = self.engine
@@ -266,6 +313,7 @@ class TetrisEnv:
     def reset(self, return_info=False):
         """TetrisEnv.reset (tetris_env.py:405-411): clear(); obs is the empty
         board (clear() returns the board before the new piece is drawn)."""
+        self._push_counts()
         self._push_rng()
         C.check(self.engine._L.st_reset(self.engine._ctx, None, self._sp))  # clear() on the env's stream
         self._started = True
@@ -334,6 +382,13 @@ class _Slot:
         self.ptrs = (vp(base), None if self.obs_f32 is None else vp(self.obs_f32.data_ptr()), vp(base + o[-2]),
                      vp(base + o[-1]), vp(base + o[1]) if lay.final else None, vp(base + o[-3]))
         self.owner = None  # weakref to the VecInfo that reads this slot
+        self.stream = -1    # the stream its last step was written on (a raw handle value; None =
+                            # the null stream; -1 = never written)
+        self.busy = 0       # copy=True pool: times it was found held since its last step
+        # the root tensor is kept: under torch.inference_mode() views do not
+        # keep their base alive, and the baseline below must count only
+        # long-lived owners
+        self._flat = flat
         self._flat_st = flat.untyped_storage()
         self._f32_st = self.obs_f32.untyped_storage() if self.obs_f32 is not None else None
         self._idle = self._refs()  # the counts while only the slot holds its tensors
@@ -357,6 +412,49 @@ class _Slot:
 
     def final_obs(self):
         return self.parts[1].view(self.lay.width, self.lay.n) if self.lay.final else None
+
+
+class _SlotPool:
+    """copy=True's output slots, oldest first.  take() reuses one of the two
+    oldest if nothing outside the pool holds it (_Slot.idle) -- callers
+    release in order, so a loop that keeps the last d steps' outputs settles
+    at d + 1 slots and then allocates nothing -- else builds a new one (the
+    oldest is dropped at `cap`).  A slot found held at the front more often
+    than the pool is long is kept for good: the pool forgets it (it is freed
+    when the caller drops it), so a few kept-forever steps do not block the
+    reuse behind them."""
+
+    def __init__(self, cap: int):
+        self.q: collections.deque = collections.deque()
+        self.cap = cap
+
+    def __len__(self):
+        return len(self.q)
+
+    def clear(self):
+        self.q.clear()
+
+    def take(self, new):
+        """(slot, reused): a released slot, or new() when none is."""
+        q = self.q
+        slot = None
+        for i in range(min(2, len(q))):
+            z = q[i]
+            if z.idle():
+                del q[i]
+                slot = z
+                break
+            z.busy += 1
+        reused = slot is not None
+        if slot is None:
+            slot = new()
+            if len(q) >= self.cap:
+                q.popleft()  # still the caller's: it is freed when they drop it
+        while q and q[0].busy > max(8, len(q)) and not q[0].idle():
+            q.popleft()
+        slot.busy = 0
+        q.append(slot)
+        return slot, reused
 
 
 class VecInfo:
@@ -455,9 +553,13 @@ class TetrisVecEnv:
     returns a fresh np.copy of the board, tetris_env.py:302): the kernel
     writes them into tensors of their own, which the env never touches
     again while the caller keeps any of them -- obs / reward / done / info,
-    a view of one, an info tensor (a slot of the last few steps is reused
-    once none of that is referenced any more, when torch's allocator would
-    hand the memory out again: `slots_reused` counts those steps).  copy=False: they live in one of two output slots
+    a view of one, an info tensor (a slot of a recent step is reused once
+    none of that is referenced any more, when torch's allocator would hand
+    the memory out again: `slots_reused` counts those steps; the pool
+    follows how many steps' outputs the caller keeps).  Outputs read on
+    another stream: call record_stream(stream) once, as Tensor.record_stream
+    for torch's allocator -- a reused slot is then written only after the
+    work queued on that stream.  copy=False: they live in one of two output slots
     that alternate, so they are overwritten two steps later (an info object
     kept longer takes a copy; the obs / reward / done tensors do not) -- the
     fast path, for loops that consume each step's outputs right away.
@@ -469,11 +571,13 @@ class TetrisVecEnv:
     anyway and sets a sticky flag in mapped host memory: no extra launch and
     no sync; the flagged step has already been applied with the bad action
     acting as idle, and the KeyError comes at the next step() after the flag
-    is seen or from check_actions().  `validate_actions=True` checks before
-    the step (the reference's immediate KeyError, before any state changes;
-    for actions already on the GPU one device->host sync per step); `False`
-    does not check (out-of-range values act as idle).  Host (numpy / list)
-    actions are always checked up front.
+    is seen or from check_actions().  `validate_actions=True` is the
+    reference's immediate KeyError, before any state changes: actions on the
+    GPU are checked by a small kernel the step launch is gated on
+    (st_gate_actions: the step changes nothing if an action is bad), and the
+    host waits for that check only, with the step already queued behind it;
+    `False` does not check (out-of-range values act as idle).  Host (numpy /
+    list) actions are always checked up front.
     """
 
     def __init__(self, num_envs: int, width=10, height=20, obs_type="ram", extend_dims=False,
@@ -510,16 +614,47 @@ class TetrisVecEnv:
         self._fin = fin
         self._lay = _SlotLayout(self.num_envs, width, height, self._want_f32, fin)
         self._slots = [] if self.copy else [_Slot(self._lay, self.device) for _ in range(2)]
-        # copy=True: the last few steps' slots, reused once the caller holds
-        # nothing of them (_Slot.idle) -- an RL loop that drops each step's
-        # outputs then pays no allocation per step; one that keeps them gets
-        # fresh slots, and the pool forgets the oldest
-        self._pool: list = []
+        # copy=True: the slots of recent steps, oldest first, reused once the
+        # caller holds nothing of them (_Slot.idle).  The pool grows to the
+        # caller's holding depth (a loop that keeps each step's outputs for d
+        # steps settles at d + 1 slots, and every step then reuses the oldest:
+        # one idle() test per step), up to _SLOT_BYTES of slots
+        slot_bytes = 4 * self._lay.total + (4 * self.num_envs * width * height if self._want_f32 else 0)
+        self._pool = _SlotPool(max(4, min(64, self._SLOT_BYTES // max(slot_bytes, 1))))
         self.slots_reused = 0
+        self._consumers: list = []  # record_stream: streams that read the outputs
         self._k = 0
         self._step_vec = self.engine._L.st_step_vec
+        self._stream_wait = self.engine._L.st_stream_wait
 
-    _POOL = 4  # copy=True: slots kept for reuse
+    _SLOT_BYTES = 1 << 30  # copy=True: most memory the slot pool keeps for reuse
+
+    def _new_slot(self):
+        return _Slot(self._lay, self.device)
+
+    def record_stream(self, stream) -> None:
+        """Declare that the outputs of this env's steps are read on `stream`
+        (a torch.cuda.Stream or a raw hipStream_t handle) -- the vector env's
+        counterpart of Tensor.record_stream, which torch's caching allocator
+        honours and this env's output slots do as well: before a step writes
+        into a slot again (a copy=True slot the caller released, or
+        copy=False's alternating slots), the env's stream waits, on the
+        device, for the work queued on every registered stream by then.  A
+        consumer on the env's own stream needs nothing (stream order)."""
+        h = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+        if all(c.value != h for c in self._consumers):
+            self._consumers.append(ctypes.c_void_p(h))
+
+    def _order_reuse(self, s: ctypes.c_void_p, prev) -> None:
+        """A slot is written on stream s again: s waits for the registered
+        consumer streams and for the stream that last wrote it (if another)."""
+        waits = [c for c in self._consumers if c.value != s.value]
+        if prev != -1 and prev != s.value:
+            waits.append(ctypes.c_void_p(prev))
+        if waits:
+            with torch.cuda.device(self.device):
+                for c in waits:
+                    C.check(self._stream_wait(s, c))
 
     def _obs(self, packed, f32):
         if self.obs_format == "packed":
@@ -554,28 +689,29 @@ class TetrisVecEnv:
 
     def step(self, actions):
         eng = self.engine
-        a = eng._actions(actions)
+        a, gated = eng._actions(actions, gate=True)
+        s = eng._stream()
         if self.copy:  # this step's outputs, the caller's from now on
-            slot = None
-            for i, z in enumerate(self._pool):
-                if z.idle():
-                    slot = self._pool.pop(i)
-                    self.slots_reused += 1
-                    break
-            if slot is None:
-                slot = _Slot(self._lay, self.device)
-                if len(self._pool) >= self._POOL:
-                    self._pool.pop(0)  # still the caller's: it is freed when they drop it
-            self._pool.append(slot)
+            slot, reused = self._pool.take(self._new_slot)
+            if reused:
+                self.slots_reused += 1
+                if self._consumers or slot.stream != s.value:  # (a reused slot was written before)
+                    self._order_reuse(s, slot.stream)
         else:
             slot = self._slots[self._k]
             self._k ^= 1
             held = slot.owner() if slot.owner is not None else None
             if held is not None:  # an info from two steps ago is still alive: it keeps a copy
                 held._detach()
+            if self._consumers or (slot.stream != -1 and slot.stream != s.value):
+                self._order_reuse(s, slot.stream)
+        slot.stream = s.value
         po, pf, pr, pd, pfin, pinfo = slot.ptrs
-        C.check(self._step_vec(eng._ctx, ctypes.c_void_p(a.data_ptr()), po, pf, pr, pd, pfin, pinfo,
-                               eng._stream()))
+        if gated:  # validate_actions=True, device actions: the step is gated (st_gate_actions)
+            eng._gate_launch(a, s)
+        C.check(self._step_vec(eng._ctx, ctypes.c_void_p(a.data_ptr()), po, pf, pr, pd, pfin, pinfo, s))
+        if gated:
+            eng._gate_wait()  # waits for the check only; raises KeyError if the step was skipped
         info = VecInfo(self, slot)
         if not self.copy:
             slot.owner = weakref.ref(info)
@@ -587,4 +723,5 @@ class TetrisVecEnv:
         self.engine.check_actions()
 
     def close(self):
+        self._pool.clear()
         self.engine.close()

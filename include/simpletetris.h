@@ -32,9 +32,10 @@ extern "C" {
 #endif
 
 /* 2: st_step_wire carries the reward's 32 bits (st_wire_words grew by one
- * word for 10x20), st_unwire_shards.  Snapshots (st_save) keep their own
+ * word for 10x20), st_unwire_shards.  3: st_gate_actions / st_gate_wait,
+ * st_stream_wait (additions only).  Snapshots (st_save) keep their own
  * format version, unchanged. */
-#define ST_ABI_VERSION 2
+#define ST_ABI_VERSION 3
 
 typedef struct st_ctx st_ctx;
 typedef void *st_stream; /* hipStream_t */
@@ -318,14 +319,37 @@ int st_check_actions(const uint8_t *d_actions, int64_t n, uint32_t *d_flag, st_s
  * valid until it is replaced; NULL turns the check off (the default). */
 int st_set_action_flag(st_ctx *ctx, uint32_t *d_flag);
 
+/* The reference's immediate KeyError (tetris_env.py:245: value_action_map
+ * [action] fails before TetrisEngine.step changes any state) for actions
+ * already on the device, without draining the stream:
+ *   st_gate_actions checks d_actions[0..n_envs) on `stream` (one small
+ *     launch) and records an event behind it; the NEXT st_step / st_step_f32 /
+ *     st_step_vec on this context is gated: if any action was outside 0..6 it
+ *     changes no env and writes no output (every env is skipped), else it is
+ *     the ordinary step.  Enqueue that step right away.
+ *   st_gate_wait then waits for the check only (the event; the gated step is
+ *     already queued behind it and runs while the host waits) and returns 1 if
+ *     an action was outside 0..6 (the step was skipped: raise KeyError), 0 if
+ *     not, < 0 on error (ST_ESTATE without a pending st_gate_actions).
+ * Other calls (st_step_wire, st_rollout, st_reset) are not gated and do not
+ * consume the gate. */
+int st_gate_actions(st_ctx *ctx, const uint8_t *d_actions, st_stream stream);
+int st_gate_wait(st_ctx *ctx);
+
 /* Runtime helpers for hosts that bind only this library (the Python package
  * uses them instead of opening the HIP runtime by name, which could load a
  * second runtime copy beside the one the kernels use):
  * st_stream_sync: hipStreamSynchronize(stream);
  * st_host_device_ptr: the device address of pinned, mapped host memory
- * (hipHostGetDevicePointer). */
+ * (hipHostGetDevicePointer);
+ * st_stream_wait: work enqueued on `waiter` after this call waits (on the
+ * device, no host wait) for the work enqueued on `signaller` before it
+ * (hipEventRecord + hipStreamWaitEvent; both streams on the current device).
+ * The vector env orders its reuse of an output slot behind the consumer
+ * streams a caller registered (TetrisVecEnv.record_stream). */
 int st_stream_sync(st_stream stream);
 int st_host_device_ptr(void *host, void **d_out);
+int st_stream_wait(st_stream waiter, st_stream signaller);
 
 /* Diagnostics: when the environment variable ST_STAMPS is set at st_create,
  * st_step runs an instrumented build of the step kernel that records

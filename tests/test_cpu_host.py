@@ -36,7 +36,7 @@ def test_host_only_abi_functions_and_constants():
     the Python binding mirrors."""
     from gym_simpletetris_amd import _lib
     L = _lib.load()
-    assert L.st_abi_version() == _lib.ABI_VERSION == 2
+    assert L.st_abi_version() == _lib.ABI_VERSION == 3
     assert L.st_export_words(10, 20) == 10 + 2 + _lib.NSTAT + _lib.MT_N + 200
     assert L.st_export_words(4, 4) == 4 + 2 + _lib.NSTAT + _lib.MT_N + 16
     # the C5 gather format: ceil((W*H + 17) / 32) words per env
@@ -47,6 +47,34 @@ def test_host_only_abi_functions_and_constants():
     defs = dict(re.findall(r"#define\s+(ST_EXPORT_\w+)\s+(\d+)u", src))
     assert int(defs["ST_EXPORT_MT"]) == _lib.EXPORT_MT and int(defs["ST_EXPORT_OBS_F32"]) == _lib.EXPORT_OBS_F32
     assert int(re.search(r"\bST_NSTAT\s*=\s*(\d+)", src).group(1)) == _lib.NSTAT  # enum constant
+    assert int(re.search(r"#define\s+ST_ABI_VERSION\s+(\d+)", src).group(1)) == _lib.ABI_VERSION
+    # argument checks that return before any GPU call
+    assert L.st_gate_actions(None, None, None) == _lib.ST_EINVAL
+    assert L.st_gate_wait(None) == _lib.ST_EINVAL
+    assert L.st_stream_wait(None, None) == _lib.ST_OK  # a stream never waits for itself
+
+
+def test_abi_mismatch_refused_unless_old_abi_opt_in(tmp_path, monkeypatch):
+    """A library of another ABI version is refused even when ST_LIB points at
+    it; only ST_AB_OLD_ABI=1 (diagnostic A/Bs) loads it, with a warning
+    (ADVICE r5)."""
+    import importlib
+    import subprocess
+    import sys
+    src = tmp_path / "old.c"
+    src.write_text("int st_abi_version(void) { return 1; }\n")
+    so = tmp_path / "libold.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)], check=True)
+    code = ("import sys; sys.path.insert(0, %r); from gym_simpletetris_amd import _lib\n"
+            "try:\n    _lib.load()\nexcept ImportError as e:\n    print('refused', e)\nelse:\n    print('loaded')")
+    pkg = os.path.join(ROOT, "gym-simpletetris_amd")
+    env = dict(os.environ, ST_LIB=str(so))
+    env.pop("ST_AB_OLD_ABI", None)
+    out = subprocess.run([sys.executable, "-c", code % pkg], env=env, capture_output=True, text=True)
+    assert out.stdout.startswith("refused") and "ABI 1" in out.stdout, out.stdout + out.stderr
+    env["ST_AB_OLD_ABI"] = "1"
+    out = subprocess.run([sys.executable, "-W", "always", "-c", code % pkg], env=env, capture_output=True, text=True)
+    assert out.stdout.startswith("loaded") and "ST_AB_OLD_ABI" in out.stderr, out.stdout + out.stderr
 
 
 def test_library_is_gfx950_code_object():

@@ -181,6 +181,10 @@ def test_bench_gpus8_direct_invocation(tmp_path):
     assert len(lines) == 1  # rank 0 prints one JSON line
     d = json.loads(lines[0])
     assert d["n_gpus"] == 8 and d["config"]["envs_total"] == 8 * 2048
+    # every rank's device identity arrived over the process group; all eight
+    # share cuda:0 on this box (ST_BENCH_SHARED_GPU), so one distinct device
+    assert d["ranks_seen"] == 8 and d["distinct_devices"] == 1
+    assert sorted(x["rank"] for x in d["topology"]["devices"]) == list(range(8))
     assert d["value"] > 0 and d["gather"]["gathers_in_timed_region"] == 20
     # the default gather format: st_step_wire's 8 rows per env, not W + 2
     assert d["gather"]["bytes_per_rank_per_step"] == 8 * 2048 * 4

@@ -121,6 +121,8 @@ def test_bench_gpus2_direct_invocation(tmp_path):
     assert len(lines) == 1  # rank 0 prints one JSON line
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["envs_total"] == 2 * 8192
+    # both ranks reported in; they share cuda:0 here (ST_BENCH_SHARED_GPU)
+    assert d["ranks_seen"] == 2 and d["distinct_devices"] == 1 and d["rccl_version"] is None
     assert d["value"] > 0 and d["gather"]["gathers_in_timed_region"] == 30
     assert d["gather"]["bytes_per_rank_per_step"] == (10 + 2) * 8192 * 4
     assert d["step_no_gather"]["value"] > 0
@@ -145,5 +147,9 @@ def test_bench_rccl_calls_one_rank(tmp_path):
     assert d["gather"]["backend"] == "nccl" and d["gather"]["gathers_in_timed_region"] == 30
     assert d["gather"]["decodes_in_timed_region_rank0"] == 30  # wire format: decoded inside the region
     assert d["value"] > 0
+    # the self-verifying topology keys the driver's N-GPU record carries
+    assert d["ranks_seen"] == 1 and d["distinct_devices"] == 1
+    assert d["rccl_version"] and not str(d["rccl_version"]).startswith("unknown")
+    assert d["topology"]["backend"] == "nccl" and d["topology"]["devices"][0]["rank"] == 0
     z = check_bench_dump(tmp_path / "c5.npz", 8192, 35)
     assert int(z["decodes_timed"]) == 30

@@ -28,9 +28,15 @@ acc, dacc = [], []
 
 
 def record():
+    global names
     b._L.st_debug_stamps(b._ctx, ctypes.c_void_p(buf.ctypes.data), buf.size)
     full = buf.reshape(nw, W).astype(np.int64)
-    acc.append(np.diff(full[:, [0, 1, 2, 3, 8, 4, 5, 6, 7]], axis=1))
+    if (full[:, 9] != 0).all():  # round 6's early stores: logic stamp 9 after them, before the lock path
+        names = ["loads+B0", "action+drop", "B1+early stores", "lock path", "late stores", "spawn-id wait",
+                 "obs+counters", "state stores issue", "store drain"]
+        acc.append(np.diff(full[:, [0, 1, 2, 9, 3, 8, 4, 5, 6, 7]], axis=1))
+    else:
+        acc.append(np.diff(full[:, [0, 1, 2, 3, 8, 4, 5, 6, 7]], axis=1))
     dacc.append(np.diff(full[:, [16 + i for i in (0, 1, 2, 10, 9, 4, 11, 6, 7)]], axis=1))
     r = full[:, 10:15].copy()
     r[:, 4] = full[:, 30]  # draw kind (written by the draw wave)
