@@ -504,9 +504,9 @@ int st_set_action_flag(st_ctx *c, uint32_t *d_flag) {
 int st_gate_actions(st_ctx *c, const uint8_t *d_actions, st_stream stream) {
     if (!c || !d_actions) return fail(ST_EINVAL, "st_gate_actions: null argument");
     DeviceGuard g(c->device);
-    if (!c->gate) {  // first use: the gate word, its mapped host copy, the event
-        ST_HIP(hipMalloc(&c->gate, sizeof(uint32_t)));
-        ST_HIP(hipMemset(c->gate, 0, sizeof(uint32_t)));
+    if (!c->gate) {  // first use: the gate words (k_gate_actions), the mapped host word, the event
+        ST_HIP(hipMalloc(&c->gate, 4 * sizeof(uint32_t)));
+        ST_HIP(hipMemset(c->gate, 0, 4 * sizeof(uint32_t)));
         ST_HIP(hipHostMalloc(&c->gate_host, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
         *c->gate_host = 0;
         void *dp = nullptr;
@@ -514,9 +514,9 @@ int st_gate_actions(st_ctx *c, const uint8_t *d_actions, st_stream stream) {
         c->gate_host_dev = static_cast<uint32_t *>(dp);
         ST_HIP(hipEventCreateWithFlags(&c->gate_ev, hipEventDisableTiming));
     }
-    c->gate_epoch = c->gate_epoch + 1u ? c->gate_epoch + 1u : 1u;  // never 0 (the words' initial value)
+    c->gate_epoch = (c->gate_epoch + 1u) & 0x7FFFFFFFu ? (c->gate_epoch + 1u) & 0x7FFFFFFFu : 1u;  // 31 bits, never 0
     hipStream_t s = (hipStream_t)stream;
-    ST_HIP(st::launch_gate_actions(d_actions, c->n, c->gate, c->gate_host_dev, c->gate_epoch, s));
+    ST_HIP(st::launch_gate_actions(d_actions, c->n, c->gate, c->gate_host_dev, c->gate_epoch, s));  // gate = words[0]
     ST_HIP(hipEventRecord(c->gate_ev, s));
     c->gate_armed = true;
     c->gate_pending = true;
@@ -527,9 +527,21 @@ int st_gate_wait(st_ctx *c) {
     if (!c) return fail(ST_EINVAL, "st_gate_wait: null context");
     if (!c->gate_pending) return fail(ST_ESTATE, "st_gate_wait without st_gate_actions");
     c->gate_pending = false;
+    // the gate kernel's last block writes epoch | bad << 31 to the mapped
+    // host word (system scope): spin on it -- the wake-up of an event wait
+    // costs more than the check itself -- and fall back to the event after
+    // ~4 million polls (a few ms: the stream was busy with earlier work)
+    const uint32_t ep = c->gate_epoch;
+    for (int i = 0; i < (1 << 22); ++i) {
+        const uint32_t v = __atomic_load_n(c->gate_host, __ATOMIC_ACQUIRE);
+        if ((v & 0x7FFFFFFFu) == ep) return (int)(v >> 31);
+        __builtin_ia32_pause();
+    }
     DeviceGuard g(c->device);
     ST_HIP(hipEventSynchronize(c->gate_ev));
-    return __atomic_load_n(c->gate_host, __ATOMIC_ACQUIRE) == c->gate_epoch ? 1 : 0;
+    const uint32_t v = __atomic_load_n(c->gate_host, __ATOMIC_ACQUIRE);
+    if ((v & 0x7FFFFFFFu) != ep) return fail(ST_EHIP, "st_gate_wait: the gate kernel finished without its answer");
+    return (int)(v >> 31);
 }
 
 int st_stream_wait(st_stream waiter, st_stream signaller) {

@@ -92,7 +92,7 @@ hipError_t launch_grayscale(const KParams &p, const uint32_t *obs, int size, int
 hipError_t launch_unwire(int W, int H, int64_t n_global, int shards, int64_t n_cap, const uint32_t *wire,
                          uint32_t *obs, int32_t *reward, uint8_t *done, hipStream_t s);
 hipError_t launch_check_actions(const uint8_t *a, int64_t n, uint32_t *flag, hipStream_t s);
-hipError_t launch_gate_actions(const uint8_t *a, int64_t n, uint32_t *gate, uint32_t *host_flag, uint32_t epoch,
+hipError_t launch_gate_actions(const uint8_t *a, int64_t n, uint32_t *words, uint32_t *host, uint32_t epoch,
                                hipStream_t s);
 hipError_t launch_gen_actions(uint8_t *out, int64_t n, int64_t t, uint64_t seed, int64_t off,
                               hipStream_t s);

@@ -510,15 +510,19 @@ __device__ __forceinline__ void mt_chunk_issue(const MtRes &rs, uint32_t mtw, bo
 // Compute and store the chunk (+ the pad copy of next[0..15] when next = A);
 // returns the chosen env's new progress.  AUX: kNT in st_step; plain in
 // rollouts, whose later steps read these words back (X operands, draws).
-template <int AUX>
+// SKIP: stores no lane of the wave needs are not issued (wave-uniform
+// branches on c.l / c.cur / c.pg; st_step, where no load follows them).
+template <int AUX, bool SKIP = false>
 __device__ __forceinline__ int mt_chunk_store(const MtRes &rs, int lane, const MtChunk &c) {
     const int k = c.pg + lane;
     const bool on = c.l >= 0 && k < kMtN;
     const uint32_t v = c.x ^ mt_mix(c.a0, c.a1);
     const uint32_t nb = c.cur ? 0u : kMtB;
-    __builtin_amdgcn_raw_buffer_store_b32(v, rs.r, on ? c.base + 4u * (nb + (uint32_t)k) : kOff, 0, AUX);
-    __builtin_amdgcn_raw_buffer_store_b32(v, rs.r, on && c.cur && k < kMtWin ? c.base + 4u * (kMtPad + (uint32_t)k) : kOff,
-                                          0, AUX);
+    if (!SKIP || c.l >= 0)
+        __builtin_amdgcn_raw_buffer_store_b32(v, rs.r, on ? c.base + 4u * (nb + (uint32_t)k) : kOff, 0, AUX);
+    if (!SKIP || (c.l >= 0 && c.cur && c.pg < kMtWin))
+        __builtin_amdgcn_raw_buffer_store_b32(v, rs.r, on && c.cur && k < kMtWin ? c.base + 4u * (kMtPad + (uint32_t)k) : kOff,
+                                              0, AUX);
     return c.pg + kWave < kMtN ? c.pg + kWave : kMtN;
 }
 
@@ -1400,6 +1404,18 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
 #ifndef ST_EARLY
 #define ST_EARLY 0
 #endif
+    // SKIP (round 6): a store instruction at the end of a wave's chain that
+    // no lane needs this step is not issued at all (a wave-uniform branch on
+    // its ballot) instead of issued with an out-of-range offset on every
+    // lane: masked-off store instructions still take their turn in the CU's
+    // memory pipeline behind the other waves' stores (round 5's ablations:
+    // the 7 lock-path counter stores cost 9% of the step).  Only stores after
+    // a wave's last wait on a load: a store skipped on some path makes the
+    // compiler's vmcnt bookkeeping conservative for later loads.
+#ifndef ST_SKIP
+#define ST_SKIP 0
+#endif
+    constexpr bool SKIP = ST_SKIP && KSTEPS == 1;
     constexpr bool EARLY = ST_EARLY && KSTEPS == 1 && !VEC && DO_L;
     [[maybe_unused]] const bool wide_obs1 = OVP && (p.n & 3) == 0 && e0 + kWave <= p.n &&
                                             (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0 &&
@@ -1587,6 +1603,17 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         }
     }
     ST_STAMP(3);
+    // SKIP_BOARD (round 6): the logic wave takes its late-loaded counters
+    // here, right after the lock path (issued before B1, they have long
+    // arrived), so that no load is waited on after its stores begin: every
+    // store from here on may then be skipped by a wave-uniform branch without
+    // making a later vmcnt wait conservative -- the board row groups no lane
+    // dirtied are not stored at all
+#ifndef ST_SKIP_BOARD
+#define ST_SKIP_BOARD 0
+#endif
+    constexpr bool SKIP_BOARD = ST_SKIP_BOARD && SKIP && LCL && DO_L;
+    if constexpr (SKIP_BOARD) asm volatile("" ::"v"(lcv[0]), "v"(lcv[1]), "v"(lcv[2]), "v"(lcv[3]), "v"(lcv[4]));
 
     const bool reset_now = died && p.autoreset == ST_AUTORESET_SAME_STEP;
     // a lock consumes the preview (spawn, or the same-step reset's new piece);
@@ -1611,6 +1638,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         const bool late = real && (!EARLY || locknow);  // EARLY: the other lanes stored theirs already
         __builtin_amdgcn_raw_buffer_store_b32(rew, rr, late ? (uint32_t)e * 4u : kOff, 0, kRD);
         __builtin_amdgcn_raw_buffer_store_b8((char)(died ? 1 : 0), rd, late ? (uint32_t)e : kOff, 0, kRD);
+        if constexpr (KSTEPS == 1) ST_STAMP(10);  // (logic wave, round 6: reward / done stores issued)
     }
     if constexpr (DO_L && KSTEPS == 1) {
         // The post-step board never depends on the spawned piece either (a
@@ -1667,6 +1695,10 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("" : "+v"(km.x), "+v"(km.y), "+v"(km.z), "+v"(km.w), "+v"(bd4.x), "+v"(bd4.y), "+v"(bd4.z),
                      "+v"(bd4.w));
+        if constexpr (STAMP) {  // (round 6: the row reads arrived, before the first store)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            ST_STAMP(11);
+        }
         const uint32_t bdl = (bd4.x | bd4.y | bd4.z | bd4.w) >> lrow;
         // the board array as one resource: byte offsets < W * stride * 4 <= 2^31
         const auto rb = buf_rsrc(p.board, (uint32_t)W * (uint32_t)sd * 4u);
@@ -1707,7 +1739,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 v.w &= km.w;
                 // row 4q + lrow; padding rows (>= W) are never dirty
                 const bool dirty = ((bdl >> (4 * q)) & 1u) && 4 * q + lrow < W && !(kAblate & 4096u);
-                buf_store16<kST>(rb, dirty ? boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff, v);
+                if (!SKIP_BOARD || __ballot(dirty))
+                    buf_store16<kST>(rb, dirty ? boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff, v);
             }
         }
         // (below: the ragged / unaligned obs path and the float32 writer read
@@ -1759,7 +1792,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         // this step's next-generation chunk (its operands arrived long ago);
         // its env's progress advances unless that env's own draw switched
         // generations (finishing the successor itself: same words)
-        const int chunk_pg = mt_chunk_store<KSTEPS == 1 ? kST : 0>(mrs, lane, chunk);
+        const int chunk_pg = mt_chunk_store<KSTEPS == 1 ? kST : 0, SKIP>(mrs, lane, chunk);
         const bool chunk_me = lane == chunk.l;
         ST_STAMP(4);
         if constexpr (STAMP) {  // 1: a draw started a generation, 2: a draw ran past its 8 words
@@ -1791,11 +1824,14 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             const uint32_t eo = (uint32_t)e * 4u;
             // (ablation 2048: the lock-path counter stores dropped, timing only)
             const bool cst = !(kAblate & (2048u | 32768u));
-            __builtin_amdgcn_raw_buffer_store_b32(
-                mt_out, rs, cst && !(kAblate & 131072u) && (dr || chunk_me) ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff, 0, kST);
-            __builtin_amdgcn_raw_buffer_store_b32(
-                (uint32_t)csid, rs, cst && !(kAblate & 65536u) && dr
-                                        ? eo + (uint32_t)(ST_STAT_COUNT0 + sid) * (uint32_t)sd * 4u : kOff, 0, kST);
+            const bool mst = cst && !(kAblate & 131072u) && (dr || chunk_me);
+            const bool kst = cst && !(kAblate & 65536u) && dr;
+            if (!SKIP || __ballot(mst))
+                __builtin_amdgcn_raw_buffer_store_b32(
+                    mt_out, rs, mst ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff, 0, kST);
+            if (!SKIP || __ballot(kst))
+                __builtin_amdgcn_raw_buffer_store_b32(
+                    (uint32_t)csid, rs, kst ? eo + (uint32_t)(ST_STAT_COUNT0 + sid) * (uint32_t)sd * 4u : kOff, 0, kST);
             if constexpr (VEC) {  // st_step_vec's info snapshot: the shape counts after the step
                 const auto ri = buf_rsrc(p.info, (uint32_t)ST_NSTAT * (uint32_t)p.n * 4u);
 #pragma unroll
@@ -1871,6 +1907,9 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
             const uint32_t eo = (uint32_t)e * 4u;
             auto put = [&](int r, int32_t v, bool on) {
+                if constexpr (SKIP) {
+                    if (!__ballot(on)) return;  // no lane changed this row: no store instruction
+                }
                 __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, on ? eo + (uint32_t)r * (uint32_t)sd * 4u : kOff,
                                                       0, kST);
             };
@@ -2063,7 +2102,9 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         // st_set_action_flag's sticky word: only lanes that saw a bad action
         // store (a raw buffer store with an out-of-range offset elsewhere, no
         // branch); a null flag has an empty range, so nothing is written
-        __builtin_amdgcn_raw_buffer_store_b32(1u, buf_rsrc(p.act_flag, 4u), bad_act ? 0u : kOff, 0, 0);
+        // (SKIP: the store is issued only in a wave that saw a bad action)
+        if (!(ST_SKIP && KSTEPS == 1) || __ballot(bad_act))
+            __builtin_amdgcn_raw_buffer_store_b32(1u, buf_rsrc(p.act_flag, 4u), bad_act ? 0u : kOff, 0, 0);
     }
     if constexpr (KSTEPS != 1 && DO_L) {
         // 32-bit buffer offsets: 64-bit row offsets shared with the prologue
@@ -2133,6 +2174,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 slot[11] = __builtin_amdgcn_s_memrealtime();
                 slot[12] = __builtin_amdgcn_s_getreg(0xF804);  // HW_ID
                 slot[13] = __builtin_amdgcn_s_getreg(0xF814);  // XCC_ID
+                slot[14] = tstamp[10];  // round 6: reward / done issued
+                slot[15] = tstamp[11];  // round 6: the store phase's LDS reads arrived
             }
         }
     }
@@ -2958,8 +3001,16 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             if (lane == last_l && cur == last_cur && last_pg > pg) pg = last_pg;
             mt_chunk_issue_pc(orm, (w >> 31) != 0u && pg < kMtN, pg, cur, lane, ch);
         };
+        // RO_SKIP (round 6): the output wave issues the chunk's pad-copy store
+        // and a step's episode-counter stores only in waves where a lane
+        // needs them (wave-uniform branches), after the chunk's operand
+        // wait, so every vmcnt count stays exact
+#ifndef ST_RO_SKIP
+#define ST_RO_SKIP 0
+#endif
+        constexpr bool RO_SKIP = ST_RO_SKIP;
         auto chunk_done = [&]() {
-            const int npg = mt_chunk_store<0>(orm, lane, ch);
+            const int npg = mt_chunk_store<0, RO_SKIP>(orm, lane, ch);
             if (ch.l >= 0) {
                 last_l = ch.l;
                 last_cur = ch.cur;
@@ -3088,32 +3139,48 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                             *reinterpret_cast<uint4 *>(&OV[(4 * q + lrow + kPad) * kWave + lcc]) =
                                 make_uint4(0u, 0u, 0u, 0u);
                 }
+                // a reset's episode counters of step t (read from the hand-off
+                // buffer before fq is raised; stored below)
+                const uint32_t dn = sm.dn[t & 1][lane];
+                const bool rs_now = dn != 0u && p.autoreset == ST_AUTORESET_SAME_STEP;
+                uint32_t epv[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) epv[k] = sm.ep[t & 1][k][lane];
                 {
-                    // reward / done of step t (and a reset's episode counters): branch-free
-                    // stores, out-of-range offsets where there is nothing to store
+                    // reward / done of step t: branch-free stores, out-of-range
+                    // offsets where there is nothing to store
                     const auto rr = buf_rsrc(p.reward ? p.reward + (int64_t)t * p.n : nullptr, (uint32_t)p.n * 4u);
                     const auto rd = buf_rsrc(p.done ? p.done + (int64_t)t * p.n : nullptr, (uint32_t)p.n);
-                    const uint32_t dn = sm.dn[t & 1][lane];
                     if (!(kAblate & 64u)) {
                         __builtin_amdgcn_raw_buffer_store_b32(sm.rw[t & 1][lane], rr, real ? (uint32_t)e * 4u : kOff, 0, kRD);
                         __builtin_amdgcn_raw_buffer_store_b8((char)dn, rd, real ? (uint32_t)e : kOff, 0, kRD);
-                        const bool rs_now = dn != 0u && p.autoreset == ST_AUTORESET_SAME_STEP;
-                        const auto rs = buf_rsrc(p.stats, (uint32_t)ST_NSTAT * (uint32_t)sd * 4u);
-                        const uint32_t eo = (uint32_t)e * 4u;
-                        constexpr int kEpRow[4] = {ST_STAT_EP_TIME, ST_STAT_EP_SCORE, ST_STAT_EP_LINES, ST_STAT_EP_HOLES};
-#pragma unroll
-                        for (int k = 0; k < 4; ++k)
-                            __builtin_amdgcn_raw_buffer_store_b32(sm.ep[t & 1][k][lane], rs,
-                                                                  rs_now ? eo + (uint32_t)kEpRow[k] * (uint32_t)sd * 4u : kOff, 0, kST);
                     }
                 }
+                auto ep_store = [&]() {
+                    if (kAblate & 64u) return;
+                    if constexpr (RO_SKIP) {
+                        if (!__ballot(rs_now)) return;  // no env of the wave was reset in step t
+                    }
+                    const auto rs = buf_rsrc(p.stats, (uint32_t)ST_NSTAT * (uint32_t)sd * 4u);
+                    const uint32_t eo = (uint32_t)e * 4u;
+                    constexpr int kEpRow[4] = {ST_STAT_EP_TIME, ST_STAT_EP_SCORE, ST_STAT_EP_LINES, ST_STAT_EP_HOLES};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        __builtin_amdgcn_raw_buffer_store_b32(epv[k], rs,
+                                                              rs_now ? eo + (uint32_t)kEpRow[k] * (uint32_t)sd * 4u : kOff, 0, kST);
+                };
+                if constexpr (!RO_SKIP) ep_store();
                 if constexpr (!EARLY)
                     if (lane == 0) lds_flag_set(&sm.fq, (uint32_t)t + 1u);  // the logic wave may change the planes
                 stamp(4);
                 if constexpr (CHO) {
                     if constexpr (decltype(dn_c)::value) chunk_done();  // the previous chunk (none at first: ch.l < 0)
                     stamp(5);
+                    // (RO_SKIP: after the chunk's operand wait, before the next chunk's loads)
+                    if constexpr (RO_SKIP) ep_store();
                     if constexpr (decltype(nx_c)::value) chunk_next();
+                } else if constexpr (RO_SKIP) {
+                    ep_store();
                 }
                 stamp(2);
             };
@@ -3758,26 +3825,42 @@ __global__ __launch_bounds__(256) void k_check_actions(const uint8_t *__restrict
     if (bad) flag[0] = 1u;
 }
 
-// st_gate_actions: the same test, writing the call's epoch (never 0) to the
-// context's gate word and to the caller-visible host word where any action
-// is outside 0..6.  Every writer stores the same value, so plain stores
-// suffice, and the words need no reset between calls: a gated step compares
-// the gate with its own epoch (KParams::gate_epoch).
-__global__ __launch_bounds__(256) void k_gate_actions(const uint8_t *__restrict__ a, int64_t n, uint32_t *gate,
-                                                      uint32_t *host_flag, uint32_t epoch) {
-    const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
-    if (i0 >= n) return;
+// st_gate_actions: the same test over all n actions, reduced to one answer
+// per call: words[0] = the gate the next step reads (the epoch if an action
+// is outside 0..6, else 0), words[1] = blocks finished (the last one resets
+// it), words[2] = the epoch once any block saw a bad action (epoch-tagged, so
+// no word needs clearing between calls).  The last block publishes the gate
+// and writes the host word -- epoch | bad << 31, system scope -- which
+// st_gate_wait spins on: the host waits for this kernel alone.  Every
+// atomic is a per-lane global atomic (no scalar-cache write).
+__global__ __launch_bounds__(256) void k_gate_actions(const uint8_t *__restrict__ a, int64_t n, uint32_t *words,
+                                                      uint32_t *host, uint32_t epoch) {
+    auto over6 = [](uint32_t w) { return ((((w & 0x7F7F7F7Fu) + 0x79797979u) | w) & 0x80808080u) != 0u; };
     bool bad = false;
-    if (i0 + 16 <= n && (reinterpret_cast<uintptr_t>(a + i0) & 15u) == 0) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(a + i0);
-        auto over6 = [](uint32_t w) { return ((((w & 0x7F7F7F7Fu) + 0x79797979u) | w) & 0x80808080u) != 0u; };
-        bad = over6(v.x) || over6(v.y) || over6(v.z) || over6(v.w);
-    } else {
-        for (int64_t i = i0; i < n && i < i0 + 16; ++i) bad = bad || a[i] > 6;
+    const int64_t step = (int64_t)gridDim.x * blockDim.x * 16;
+    for (int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; i0 < n; i0 += step) {
+        if (i0 + 16 <= n && (reinterpret_cast<uintptr_t>(a + i0) & 15u) == 0) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(a + i0);
+            bad = bad || over6(v.x) || over6(v.y) || over6(v.z) || over6(v.w);
+        } else {
+            for (int64_t i = i0; i < n && i < i0 + 16; ++i) bad = bad || a[i] > 6;
+        }
     }
-    if (bad) {
-        gate[0] = epoch;
-        host_flag[0] = epoch;
+    // a wave that saw one tags words[2] and waits for the atomic's return, so
+    // the tag is performed at L2 before its block counts itself done
+    if (__ballot(bad) && (threadIdx.x & (kWave - 1)) == 0) {
+        const uint32_t old = __hip_atomic_exchange(&words[2], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("" ::"v"(old));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t done = __hip_atomic_fetch_add(&words[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (done == gridDim.x - 1) {  // the last block: every tag is in
+            const bool any = __hip_atomic_load(&words[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+            words[0] = any ? epoch : 0u;
+            __hip_atomic_store(&words[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(host, epoch | (any ? 0x80000000u : 0u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -4064,11 +4147,12 @@ hipError_t launch_check_actions(const uint8_t *a, int64_t n, uint32_t *flag, hip
     return hipGetLastError();
 }
 
-hipError_t launch_gate_actions(const uint8_t *a, int64_t n, uint32_t *gate, uint32_t *host_flag, uint32_t epoch,
+hipError_t launch_gate_actions(const uint8_t *a, int64_t n, uint32_t *words, uint32_t *host, uint32_t epoch,
                                hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_gate_actions, dim3((unsigned)((n + 16 * 256 - 1) / (16 * 256))), dim3(256), 0, s, a, n,
-                       gate, host_flag, epoch);
+    // at most 64 blocks of 256 threads, 16 actions per thread and pass
+    const int64_t want = (n + 16 * 256 - 1) / (16 * 256);
+    const unsigned blocks = (unsigned)(want < 1 ? 1 : (want > 64 ? 64 : want));
+    hipLaunchKernelGGL(k_gate_actions, dim3(blocks), dim3(256), 0, s, a, n, words, host, epoch);
     return hipGetLastError();
 }
 

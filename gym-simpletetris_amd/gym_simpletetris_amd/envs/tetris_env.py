@@ -391,15 +391,17 @@ class _Slot:
         self._flat = flat
         self._flat_st = flat.untyped_storage()
         self._f32_st = self.obs_f32.untyped_storage() if self.obs_f32 is not None else None
+        self._flat_cd = self._flat_st._cdata
         self._idle = self._refs()  # the counts while only the slot holds its tensors
 
     def _refs(self):
         """Python references to the tensors step() hands out, and the owners
         of the two allocations (every view of them, the caller's included)."""
-        f32 = self.obs_f32 is not None  # (None's own count moves all the time: not counted)
-        return (sys.getrefcount(self.obs), sys.getrefcount(self.reward), sys.getrefcount(self.done),
-                sys.getrefcount(self.obs_f32) if f32 else 0, torch._C._storage_Use_Count(self._flat_st._cdata),
-                torch._C._storage_Use_Count(self._f32_st._cdata) if f32 else 0)
+        g, use = sys.getrefcount, torch._C._storage_Use_Count
+        if self.obs_f32 is None:  # (None's own count moves all the time: not counted)
+            return g(self.obs), g(self.reward), g(self.done), use(self._flat_cd)
+        return (g(self.obs), g(self.reward), g(self.done), g(self.obs_f32), use(self._flat_cd),
+                use(self._f32_st._cdata))
 
     def idle(self) -> bool:
         """Nothing outside the slot still holds its outputs (no returned
@@ -436,6 +438,16 @@ class _SlotPool:
 
     def take(self, new):
         """(slot, reused): a released slot, or new() when none is."""
+        q = self.q
+        if q:  # the common case: the oldest slot was released -- it goes to the back
+            z = q[0]
+            if z.idle():
+                q.rotate(-1)
+                z.busy = 0
+                return z, True
+        return self._take_slow(new)
+
+    def _take_slow(self, new):
         q = self.q
         slot = None
         for i in range(min(2, len(q))):

@@ -35,6 +35,10 @@ def record():
         names = ["loads+B0", "action+drop", "B1+early stores", "lock path", "late stores", "spawn-id wait",
                  "obs+counters", "state stores issue", "store drain"]
         acc.append(np.diff(full[:, [0, 1, 2, 9, 3, 8, 4, 5, 6, 7]], axis=1))
+    elif (full[:, 14] != 0).all() and (full[:, 15] != 0).all():  # round 6's split of the early-store phase
+        names = ["loads+B0", "action+drop", "B1+lock path", "reward/done issue", "paint+LDS reads",
+                 "obs+board stores", "spawn-id wait", "obs+counters", "state stores issue", "store drain"]
+        acc.append(np.diff(full[:, [0, 1, 2, 3, 14, 15, 8, 4, 5, 6, 7]], axis=1))
     else:
         acc.append(np.diff(full[:, [0, 1, 2, 3, 8, 4, 5, 6, 7]], axis=1))
     dacc.append(np.diff(full[:, [16 + i for i in (0, 1, 2, 10, 9, 4, 11, 6, 7)]], axis=1))
