@@ -44,7 +44,8 @@ struct KParams {
                         // draw wave's count / MT-word store only; 262144 = the draw
                         // wave's count rows T J L Z not loaded, 524288 = MT windows
                         // read as zeros, 1048576 = no next-generation chunks,
-                        // 2097152 = the lock-path counter rows not loaded
+                        // 2097152 = the lock-path counter rows not loaded,
+                        // 4194304 = the store phase's LDS transposition skipped
     uint64_t *stamps;   // DIAGNOSTIC build only (env ST_STAMPS at st_create): per-wave
                         // s_memtime at 8 phase boundaries of the step kernel
     int32_t k;          // st_rollout: number of steps

@@ -1640,7 +1640,72 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         __builtin_amdgcn_raw_buffer_store_b8((char)(died ? 1 : 0), rd, late ? (uint32_t)e : kOff, 0, kRD);
         if constexpr (KSTEPS == 1) ST_STAMP(10);  // (logic wave, round 6: reward / done stores issued)
     }
-    if constexpr (DO_L && KSTEPS == 1) {
+    // OVL (round 6): the store phase with the overlay painted into the board
+    // plane itself and ONE transposed read -- half the LDS traffic of the
+    // overlay plane's (paint, keep / dirty masks, board rows and overlay
+    // rows, ~10 KB per wave, the phase's ~740 cycles in
+    // profiles/r06/stamps_fine_store_phase.txt).  The board rows then come
+    // from the obs rows: a locking env that spawned has row 0 empty under
+    // its new piece's visible cells (a spawn only overlays row 0, :277, :299),
+    // so its board is its obs with row 0 cleared; a same-step reset's board
+    // is empty; a non-locking env's board is unchanged and not stored -- so
+    // the board goes out as one dword per dirty env and row instead of 16-B
+    // groups of 4 envs.  A wave with a death without auto-reset (R8: the
+    // board is the obs minus the locked piece) takes the overlay-plane path.
+#ifndef ST_OVL
+#define ST_OVL 0
+#endif
+    constexpr bool OVL = ST_OVL && !EARLY && !VEC && KSTEPS == 1 && DO_L && LCL && WT != 0 && WT < 31;
+    if constexpr (OVL) asm volatile("" ::"v"(lcv[0]), "v"(lcv[1]), "v"(lcv[2]), "v"(lcv[3]), "v"(lcv[4]));
+    bool ovl_fast = false;
+    if constexpr (OVL) ovl_fast = !__ballot(died && !reset_now);
+    if (OVL && ovl_fast) {
+        uint2 pd = pd_pv;
+        const bool need1 = draw && !pv_ok(mt0);
+        if (__ballot(need1)) {
+            lds_flag_wait(&sm.f2, (uint32_t)t + 1u);
+            if (need1) pd = tab((int)sm.pick1[lane] * 4);
+        }
+        const uint32_t om = spawn ? pd.x : desc.x, og = spawn ? pd.y : desc.y;
+        const int ox = spawn ? W / 2 : ax, oy = spawn ? 0 : ay;
+        paint<S32>(L, lane, om, og, ox, oy, hmask);  // (a reset env's piece is in L already: idempotent)
+        // per env: the columns it changed | bit 31 = reset (empty board)
+        constexpr uint32_t kCols = (1u << (WT ? WT : 1)) - 1u;
+        sm.BD[lane] = (died ? kCols : (bdirty & kCols)) | (reset_now ? 0x80000000u : 0u);
+        wave_sync();
+        const uint4 fl4 = *reinterpret_cast<const uint4 *>(&sm.BD[lcc]);
+        uint4 rw[NBQ];
+#pragma unroll
+        for (int q = 0; q < NBQ; ++q) rw[q] = *reinterpret_cast<const uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (STAMP) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            ST_STAMP(11);
+        }
+        const auto ro = buf_rsrc(wide_obs1 ? p.obs : nullptr, (uint32_t)W * (uint32_t)p.n * 4u);
+        const auto rb = buf_rsrc(p.board, (uint32_t)W * (uint32_t)sd * 4u);
+        const uint32_t boff = ((uint32_t)e0 * 4u + loff * 4u);
+        const uint32_t fa[4] = {fl4.x, fl4.y, fl4.z, fl4.w};
+#pragma unroll
+        for (int q = 0; q < NBQ; ++q) {
+            const uint4 v = rw[q];
+            const uint4 ob = make_uint4(v.x & hmask, v.y & hmask, v.z & hmask, v.w & hmask);
+            const uint32_t ooff = ((uint32_t)e0 + (uint32_t)(4 * q + lrow) * (uint32_t)p.n + (uint32_t)lcc) * 4u;
+            buf_store16<kNT>(ro, ooff, ob);
+            const uint32_t va[4] = {ob.x, ob.y, ob.z, ob.w};
+            const int x = 4 * q + lrow;  // board row (column x of the reference's board)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const bool dirty = x < W && ((fa[i] >> x) & 1u) && !(kAblate & 4096u);
+                const uint32_t keep = (fa[i] >> 31) ? 0u : ~1u;  // reset: empty; spawn: row 0 cleared
+                __builtin_amdgcn_raw_buffer_store_b32(va[i] & keep, rb,
+                                                      dirty ? boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u + 4u * (uint32_t)i
+                                                            : kOff,
+                                                      0, kST);
+            }
+        }
+    }
+    if (DO_L && KSTEPS == 1 && !(OVL && ovl_fast)) {
         // The post-step board never depends on the spawned piece either (a
         // spawn only overlays row 0, which is empty after a non-fatal lock,
         // :277), so st_step stores it here: non-locking lanes and spawns: L; a
@@ -1671,21 +1736,35 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 // (EARLY: the non-locking lanes painted theirs before the lock path)
                 uint32_t *dst = &sm.OV[(ox + pc_dx(og, j) + kPad) * kWave + lane];
                 if constexpr (EARLY) dst = locknow ? dst : &sm.dump[lane];
-                *dst = pc_bits<S32>(om, j, oy) & hmask;
+                if (!(kAblate & 4194304u)) *dst = pc_bits<S32>(om, j, oy) & hmask;
             }
         }
+        uint4 km, bd4;
+        uint4 bw[NBQ], ow[NBQ];
+        if (kAblate & 4194304u) {
+            // (ablation 4194304: the store phase's LDS transposition skipped --
+            // no keep / dirty mask or overlay writes, no row reads; the stores
+            // take register garbage; timing only)
+            km = make_uint4(hmask, hmask, hmask, hmask);
+            bd4 = make_uint4(bdirty, bdirty, bdirty, bdirty);
+#pragma unroll
+            for (int q = 0; q < NBQ; ++q) {
+                bw[q] = make_uint4(bdirty, (uint32_t)ax, (uint32_t)ay, (uint32_t)lane);
+                ow[q] = make_uint4(desc.x, desc.y, (uint32_t)rew, (uint32_t)q);
+            }
+        } else {
         sm.KM[lane] = reset_now ? 0u : hmask;
         sm.BD[lane] = bdirty;
         wave_sync();
-        uint4 km = *reinterpret_cast<const uint4 *>(&sm.KM[lcc]);
-        uint4 bd4 = *reinterpret_cast<const uint4 *>(&sm.BD[lcc]);
-        uint4 bw[NBQ], ow[NBQ];
+        km = *reinterpret_cast<const uint4 *>(&sm.KM[lcc]);
+        bd4 = *reinterpret_cast<const uint4 *>(&sm.BD[lcc]);
 #pragma unroll
         for (int q = 0; q < NBQ; ++q) {
             if (WT || 4 * q < W) {
                 bw[q] = *reinterpret_cast<const uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]);
                 if constexpr (OVP) ow[q] = *reinterpret_cast<const uint4 *>(&sm.OV[(4 * q + lrow + kPad) * kWave + lcc]);
             }
+        }
         }
         // every read (keep / dirty masks, board and overlay rows) issued before
         // anything uses one: one LDS round trip

@@ -78,15 +78,18 @@ def test_gate_rejects_before_any_state_change(obs):
     b.close()
 
 
-def test_gate_vec_env_and_abi():
+@pytest.mark.parametrize("obs_format,copy", [("packed", True), ("f32", True), ("packed", False)])
+def test_gate_vec_env_and_abi(obs_format, copy):
     """TetrisVecEnv(validate_actions=True): a rejected step changes nothing
-    and the env continues in lockstep with an unvalidated twin; the C ABI's
-    gate calls in order (st_gate_wait without st_gate_actions: ST_ESTATE)."""
+    and the env continues in lockstep with an unvalidated twin (packed and
+    float32 obs, the reset obs / final_observation convention, both copy
+    modes); the C ABI's gate calls in order (st_gate_wait without
+    st_gate_actions: ST_ESTATE)."""
     G = _engine()
     from gym_simpletetris_amd import _lib as C
     n = 2048
-    v = G.TetrisVecEnv(n, seed=21, obs_format="packed", validate_actions=True)
-    u = G.TetrisVecEnv(n, seed=21, obs_format="packed", validate_actions=False)
+    v = G.TetrisVecEnv(n, seed=21, obs_format=obs_format, validate_actions=True, copy=copy)
+    u = G.TetrisVecEnv(n, seed=21, obs_format=obs_format, validate_actions=False, copy=copy)
     v.reset()
     u.reset()
     for t in range(60):
@@ -100,6 +103,7 @@ def test_gate_vec_env_and_abi():
         ou, ru, du, iu = u.step(acts)
         assert torch.equal(ov, ou) and torch.equal(rv, ru) and torch.equal(dv, du), t
         assert torch.equal(iv["time"], iu["time"]) and torch.equal(iv["score"], iu["score"]), t
+        assert torch.equal(iv["final_observation"], iu["final_observation"]), t
     L = v.engine._L
     assert L.st_gate_wait(v.engine._ctx) == C.ST_ESTATE
     v.close()
@@ -134,6 +138,31 @@ def test_record_stream_orders_slot_reuse():
     torch.cuda.synchronize()
     assert v.slots_reused > r0
     assert torch.equal(got, want) and torch.equal(got_r, want_r)
+    v.close()
+
+
+def test_record_stream_orders_copy_false_alternation():
+    """copy=False: the env writes a slot again two steps later; a consumer
+    registered with record_stream() that is still reading it behind queued
+    work on its own stream keeps reading the step it was given."""
+    G = _engine()
+    n = 8192
+    v = G.TetrisVecEnv(n, seed=5, obs_format="packed", copy=False)
+    side = torch.cuda.Stream()
+    v.record_stream(side)
+    v.reset()
+    for t in range(4):
+        v.step(v.engine.gen_actions(t, 2))
+    obs, rew, done, _ = v.step(v.engine.gen_actions(4, 2))
+    want = obs.clone()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        _delay()
+        got = obs.clone()
+    for t in range(5, 9):
+        v.step(v.engine.gen_actions(t, 2))  # the slot of step 4 is written again at step 6
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
     v.close()
 
 
