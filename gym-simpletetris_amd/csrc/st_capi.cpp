@@ -527,6 +527,9 @@ int st_gate_wait(st_ctx *c) {
     if (!c) return fail(ST_EINVAL, "st_gate_wait: null context");
     if (!c->gate_pending) return fail(ST_ESTATE, "st_gate_wait without st_gate_actions");
     c->gate_pending = false;
+    // the gate ends here: a step not launched by now (its launch failed, or
+    // the caller never made it) is not gated by this check later
+    c->gate_armed = false;
     // the gate kernel's last block writes epoch | bad << 31 to the mapped
     // host word (system scope): spin on it -- the wake-up of an event wait
     // costs more than the check itself -- and fall back to the event after

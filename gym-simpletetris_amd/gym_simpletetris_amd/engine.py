@@ -288,6 +288,11 @@ class TetrisBatch:
         if rc:
             raise KeyError("an action outside 0..6 (tetris_env.py:245); no env was stepped")
 
+    def _gate_abort(self) -> None:
+        """The gated step's launch failed: end the gate (st_gate_wait also
+        disarms it) so that it cannot gate a later step; its answer is moot."""
+        self._L.st_gate_wait(self._ctx)
+
     def _raise_flagged(self):
         if self._flag_np[0]:
             self._flag_np[0] = 0
@@ -331,20 +336,25 @@ class TetrisBatch:
         s = self._stream()
         if gated:  # validate_actions=True, device actions: the gated step (st_gate_actions)
             self._gate_launch(a, s)
-        # no torch.cuda.device() context: st_step selects the context's device itself
-        if obs == "f32":
-            if self.obs_f32 is None:
-                self.obs_f32 = torch.zeros((self.n, self.width, self.height),
-                                           dtype=torch.float32, device=self.device)
-            C.check(self._L.st_step_f32(self._ctx, _ptr(a), _ptr(o_t), _ptr(self.obs_f32),
+        try:
+            # no torch.cuda.device() context: st_step selects the context's device itself
+            if obs == "f32":
+                if self.obs_f32 is None:
+                    self.obs_f32 = torch.zeros((self.n, self.width, self.height),
+                                               dtype=torch.float32, device=self.device)
+                C.check(self._L.st_step_f32(self._ctx, _ptr(a), _ptr(o_t), _ptr(self.obs_f32),
+                                            _ptr(r_t), _ptr(d_t), s))
+            else:
+                C.check(self._L.st_step(self._ctx, _ptr(a), _ptr(o_t) if obs == "packed" else None,
                                         _ptr(r_t), _ptr(d_t), s))
+        except BaseException:
             if gated:
-                self._gate_wait()
-            return self.obs_f32, r_t, d_t
-        C.check(self._L.st_step(self._ctx, _ptr(a), _ptr(o_t) if obs == "packed" else None,
-                                _ptr(r_t), _ptr(d_t), s))
+                self._gate_abort()
+            raise
         if gated:
             self._gate_wait()
+        if obs == "f32":
+            return self.obs_f32, r_t, d_t
         return (o_t if obs == "packed" else None), r_t, d_t
 
     @property

@@ -721,7 +721,12 @@ class TetrisVecEnv:
         po, pf, pr, pd, pfin, pinfo = slot.ptrs
         if gated:  # validate_actions=True, device actions: the step is gated (st_gate_actions)
             eng._gate_launch(a, s)
-        C.check(self._step_vec(eng._ctx, ctypes.c_void_p(a.data_ptr()), po, pf, pr, pd, pfin, pinfo, s))
+        try:
+            C.check(self._step_vec(eng._ctx, ctypes.c_void_p(a.data_ptr()), po, pf, pr, pd, pfin, pinfo, s))
+        except BaseException:
+            if gated:
+                eng._gate_abort()
+            raise
         if gated:
             eng._gate_wait()  # waits for the check only; raises KeyError if the step was skipped
         info = VecInfo(self, slot)

@@ -78,6 +78,40 @@ def test_gate_rejects_before_any_state_change(obs):
     b.close()
 
 
+def test_gate_ends_at_wait_even_without_its_step():
+    """C ABI: a gate whose step launch failed (st_step with a null action
+    pointer: ST_EINVAL before anything is queued) ends at st_gate_wait -- the
+    next, ungated st_step is an ordinary step, not skipped by the stale
+    answer (TetrisBatch.step and TetrisVecEnv.step end a gate the same way,
+    _gate_abort, when their step launch raises)."""
+    import ctypes
+    G = _engine()
+    from gym_simpletetris_amd import _lib as C
+    n = 256
+    a = G.TetrisBatch(n, seeds=range(n), autoreset="same_step", validate_actions=False)
+    b = G.TetrisBatch(n, seeds=range(n), autoreset="same_step", validate_actions=False)
+    a.reset()
+    b.reset()
+    L, ctx, vp = a._L, a._ctx, ctypes.c_void_p
+    s = vp(torch.cuda.current_stream().cuda_stream)
+    bad = torch.full((n,), 9, dtype=torch.uint8, device=a.device)
+    assert L.st_gate_actions(ctx, vp(bad.data_ptr()), s) == 0
+    o, r, d = (torch.empty((10, n), dtype=torch.int32, device=a.device),
+               torch.empty(n, dtype=torch.int32, device=a.device), torch.empty(n, dtype=torch.uint8, device=a.device))
+    assert L.st_step(ctx, None, vp(o.data_ptr()), vp(r.data_ptr()), vp(d.data_ptr()), s) == C.ST_EINVAL
+    assert L.st_gate_wait(ctx) == 1  # the check saw the 9
+    good = b.gen_actions(0, 5).clone()
+    assert L.st_step(ctx, vp(good.data_ptr()), vp(o.data_ptr()), vp(r.data_ptr()), vp(d.data_ptr()), s) == 0
+    ob, rb, db = b.step(good)
+    torch.cuda.synchronize()
+    assert torch.equal(o, ob) and torch.equal(r, rb) and torch.equal(d.bool(), db.bool())
+    sa, sb = _state(a), _state(b)
+    for k in sa:
+        assert np.array_equal(sa[k], sb[k]), k
+    a.close()
+    b.close()
+
+
 @pytest.mark.parametrize("obs_format,copy", [("packed", True), ("f32", True), ("packed", False)])
 def test_gate_vec_env_and_abi(obs_format, copy):
     """TetrisVecEnv(validate_actions=True): a rejected step changes nothing
