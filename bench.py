@@ -265,8 +265,26 @@ def rank_topology(dev, rank: int, local_rank: int, world: int, use_dist: bool, b
             rccl = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
         except Exception as ex:  # noqa: BLE001 (reported, not fatal)
             rccl = f"unknown ({ex})"
-    return {"ranks_seen": len(devices), "distinct_devices": len({d["device_key"] for d in devices}),
+    return {"ranks_seen": len(devices), "distinct_devices": distinct_devices(devices),
             "backend": backend if use_dist else None, "rccl_version": rccl, "devices": devices}
+
+
+def distinct_devices(devices: list) -> int:
+    """Distinct physical GPUs among the ranks' identities: the largest count
+    any identity every rank reported gives -- UUIDs (all-zero ones ignored),
+    then host + PCI domain:bus:device -- so that one missing or degenerate
+    field cannot make distinct GPUs look shared (two ranks on one GPU agree on
+    every field); the device_key alone when neither is there."""
+    counts = []
+    uu = [d.get("uuid") for d in devices]
+    if all(u and u.strip("0-") for u in uu):
+        counts.append(len(set(uu)))
+    if all(d.get("pci_bus_id") is not None for d in devices):
+        counts.append(len({(d.get("host"), d.get("pci_domain_id"), d["pci_bus_id"], d.get("pci_device_id"))
+                           for d in devices}))
+    if not counts:
+        counts.append(len({d["device_key"] for d in devices}))
+    return max(counts)
 
 
 def spawn_ranks(n: int) -> int:

@@ -317,3 +317,27 @@ def test_dlpack_producer_passes_through_without_copy():
     assert _from_dlpack(t) is t
     a = np.arange(3)
     assert _from_dlpack(a) is a
+
+
+def test_bench_distinct_devices_counts_physical_gpus():
+    """bench.py --gpus N refuses to run when fewer distinct GPUs than ranks
+    answer; the count must not mistake distinct GPUs for one when a field is
+    degenerate (all-zero UUIDs), nor one shared GPU for several."""
+    import bench
+
+    def ident(uuid, bus, host="h"):
+        d = {"host": host, "pci_domain_id": "0", "pci_bus_id": bus, "pci_device_id": "0"}
+        if uuid is not None:
+            d["uuid"] = uuid
+        d["device_key"] = "uuid:%s" % uuid if uuid else "pci:%s" % bus
+        return d
+    shared = [ident("35383437-6461", "139")] * 8
+    assert bench.distinct_devices(shared) == 1
+    distinct = [ident("u%d" % i, str(100 + i)) for i in range(8)]
+    assert bench.distinct_devices(distinct) == 8
+    zero_uuid = [ident("00000000-0000-0000-0000-000000000000", str(100 + i)) for i in range(8)]
+    assert bench.distinct_devices(zero_uuid) == 8
+    same_uuid_distinct_pci = [ident("35383437", str(100 + i)) for i in range(4)]
+    assert bench.distinct_devices(same_uuid_distinct_pci) == 4
+    no_fields = [{"host": "h", "device_key": "idx:h:None:%d" % i} for i in range(2)]
+    assert bench.distinct_devices(no_fields) == 2
