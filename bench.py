@@ -325,10 +325,11 @@ def main():
     ap.add_argument("--n-envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c3")
     ap.add_argument("--obs", choices=("packed", "f32"), default="packed")
-    ap.add_argument("--launch", choices=("graph", "eager"), default="eager",
-                    help="timed steps as K eager st_step launches, or one hipGraph of them "
-                         "(measured: graph replay 2.5%% slower at K=4000, noisier at K=20; "
-                         "profiles/r02_launch_ab.jsonl)")
+    ap.add_argument("--launch", choices=("native", "eager", "graph"), default="native",
+                    help="timed steps as K st_step kernel launches enqueued by ONE st_step_n call "
+                         "(native: the library's own launch loop, no Python between launches), by K "
+                         "ctypes st_step calls (eager), or as one hipGraph of them (graph replay: "
+                         "2.5%% slower at K=4000, profiles/r02_launch_ab.jsonl)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--gather-format", choices=("wire", "rows"), default="wire",
                     help="C5 (--gpus > 1, packed obs): what each step gathers to rank 0 -- st_step_wire's "
@@ -574,12 +575,23 @@ def main():
             else:
                 self.fn = L.st_step
                 self.args = [(ctx, self.aptr[t], po, pr, pd, sp) for t in range(WU + K)]
+            # --launch native: every step's action pointer in one host array,
+            # so K steps are one st_step_n call (K kernel launches from C)
+            self.aarr = (ctypes.c_void_p * (WU + K))(*[a.value for a in self.aptr])
+            self.nargs = (ctx, po, self.pf, pr, pd, sp)
 
         def launch(self, t):
             C.check(self.fn(*self.args[t]))
 
         def launch_range(self, t0, t1):
-            """Steps t0 .. t1-1, one ctypes st_step call each."""
+            """Steps t0 .. t1-1: one st_step kernel launch each, enqueued by
+            one st_step_n call (--launch native) or one ctypes st_step call
+            per step (eager; graph capture)."""
+            if args.launch == "native":
+                ctx, po, pf, pr, pd, sp_ = self.nargs
+                C.check(self.eng._L.st_step_n(ctx, ctypes.addressof(self.aarr) + t0 * ctypes.sizeof(ctypes.c_void_p),
+                                              t1 - t0, po, pf, pr, pd, sp_))
+                return
             fn, rc = self.fn, 0
             for a in self.args[t0:t1]:
                 rc = rc or fn(*a)  # stop at the first failure and report its code
@@ -743,7 +755,7 @@ def main():
             return out
 
         def runner(self):
-            if args.launch == "eager":
+            if args.launch != "graph":
                 return (lambda: self.launch_range(WU, WU + K)), None
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
@@ -885,8 +897,10 @@ def main():
             "envs_total": head.n_global,
             "board": f"{W}x{H}",
             "obs": args.obs,
-            "launch": ("hipGraph of K st_step launches" if args.launch == "graph"
-                       else "K eager st_step launches"),
+            "launch": {"graph": "hipGraph of K st_step launches",
+                       "eager": "K eager st_step launches, one ctypes call each",
+                       "native": "K st_step launches enqueued by one st_step_n call (the library's launch loop)"}[
+                args.launch],
             "parallelism": f"env-shard x{world}",
             "hip_force_dev_kernarg": os.environ.get("HIP_FORCE_DEV_KERNARG"),
             "hip_force_dev_kernarg_from": "environment" if KERNARG_FROM_ENV else "bench.py (tune_runtime opt-in)",
@@ -1160,7 +1174,13 @@ def clear_heavy(head, cfg_kw, C, ShardedTetris, timed, roofline, kname_of, dev, 
         for t in range(WU):
             C.check(L.st_step(ce._ctx, gptr[t], po, pr, pd, sp))
     torch.cuda.synchronize(dev)
+    garr = (ctypes.c_void_p * (WU + K))(*[a.value for a in gptr])
+
     def run_eager():
+        if launch == "native":  # the headline's launch path: one st_step_n call
+            C.check(L.st_step_n(ce._ctx, ctypes.addressof(garr) + WU * ctypes.sizeof(ctypes.c_void_p), K, po, None,
+                                pr, pd, sp))
+            return
         for t in range(WU, WU + K):
             C.check(L.st_step(ce._ctx, gptr[t], po, pr, pd, sp))
     g = None

@@ -238,6 +238,23 @@ int st_step_f32(st_ctx *c, const uint8_t *d_actions, uint32_t *d_obs, float *d_o
     return step_impl(c, d_actions, d_obs, d_obs_f32, d_reward, d_done, stream);
 }
 
+int st_step_n(st_ctx *c, const uint8_t *const *d_actions, int64_t k, uint32_t *d_obs, float *d_obs_f32,
+              int32_t *d_reward, uint8_t *d_done, st_stream stream) {
+    if (!c) return fail(ST_EINVAL, "st_step_n: null context");
+    if (k <= 0) return ST_OK;
+    if (!d_actions) return fail(ST_EINVAL, "st_step_n: null action pointer array");
+    for (int64_t i = 0; i < k; ++i)
+        if (!d_actions[i]) return fail(ST_EINVAL, "st_step_n: null action pointer");
+    // one device switch for the whole loop (step_impl's own guard then finds
+    // the device current and sets nothing)
+    DeviceGuard g(c->device);
+    for (int64_t i = 0; i < k; ++i) {
+        const int rc = step_impl(c, d_actions[i], d_obs, d_obs_f32, d_reward, d_done, stream);
+        if (rc != ST_OK) return rc;
+    }
+    return ST_OK;
+}
+
 int st_step_vec(st_ctx *c, const uint8_t *d_actions, uint32_t *d_obs, float *d_obs_f32, int32_t *d_reward,
                 uint8_t *d_done, uint32_t *d_final_obs, int32_t *d_info, st_stream stream) {
     // final_obs is part of the obs output: without d_obs the kernel's two store

@@ -510,19 +510,15 @@ __device__ __forceinline__ void mt_chunk_issue(const MtRes &rs, uint32_t mtw, bo
 // Compute and store the chunk (+ the pad copy of next[0..15] when next = A);
 // returns the chosen env's new progress.  AUX: kNT in st_step; plain in
 // rollouts, whose later steps read these words back (X operands, draws).
-// SKIP: stores no lane of the wave needs are not issued (wave-uniform
-// branches on c.l / c.cur / c.pg; st_step, where no load follows them).
-template <int AUX, bool SKIP = false>
+template <int AUX>
 __device__ __forceinline__ int mt_chunk_store(const MtRes &rs, int lane, const MtChunk &c) {
     const int k = c.pg + lane;
     const bool on = c.l >= 0 && k < kMtN;
     const uint32_t v = c.x ^ mt_mix(c.a0, c.a1);
     const uint32_t nb = c.cur ? 0u : kMtB;
-    if (!SKIP || c.l >= 0)
-        __builtin_amdgcn_raw_buffer_store_b32(v, rs.r, on ? c.base + 4u * (nb + (uint32_t)k) : kOff, 0, AUX);
-    if (!SKIP || (c.l >= 0 && c.cur && c.pg < kMtWin))
-        __builtin_amdgcn_raw_buffer_store_b32(v, rs.r, on && c.cur && k < kMtWin ? c.base + 4u * (kMtPad + (uint32_t)k) : kOff,
-                                              0, AUX);
+    __builtin_amdgcn_raw_buffer_store_b32(v, rs.r, on ? c.base + 4u * (nb + (uint32_t)k) : kOff, 0, AUX);
+    __builtin_amdgcn_raw_buffer_store_b32(v, rs.r, on && c.cur && k < kMtWin ? c.base + 4u * (kMtPad + (uint32_t)k) : kOff,
+                                          0, AUX);
     return c.pg + kWave < kMtN ? c.pg + kWave : kMtN;
 }
 
@@ -1361,10 +1357,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         for (int i = 1; i < 7; ++i) csid = s0 == i ? cnt[i] : csid;
         dpar = draw_par(cnt);
     }
-    [[maybe_unused]] uint64_t lockball = 0;  // the wave's locking lanes
     if constexpr (DO_L) {
         const uint64_t m = __ballot(locknow);
-        lockball = m;
         if (lane == 0) {
             sm.lockm[t & 1][0] = (uint32_t)m;
             sm.lockm[t & 1][1] = (uint32_t)(m >> 32);
@@ -1392,80 +1386,10 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
     // (ablation 524288: the window's words read as zeros, no traffic -- timing only)
     if constexpr (DO_D) mt_pre_load<kWin>(mrs, mtst, want_pre && !(kAblate & 524288u), pre);
 
-    // ---------------- st_step: early stores (round 6) ----------------
-    // Everything a lane that does not lock outputs is final once its action
-    // phase is done: reward (reward_step's 1 or 0, :256), done = 0, the clock,
-    // the piece word, and its obs -- the unchanged board with the piece at
-    // its new position (:301-302).  Those stores go out here, before the lock
-    // path, instead of in the grid-wide store burst after it: the memory
-    // system is idle while the waves run their lock paths.  The obs rows go
-    // as 16-B groups of 4 envs, so a group holding a locking env waits for
-    // the late pass.  EARLY = 0 keeps the round-5 schedule (A/B builds).
-#ifndef ST_EARLY
-#define ST_EARLY 0
-#endif
-    // SKIP (round 6): a store instruction at the end of a wave's chain that
-    // no lane needs this step is not issued at all (a wave-uniform branch on
-    // its ballot) instead of issued with an out-of-range offset on every
-    // lane: masked-off store instructions still take their turn in the CU's
-    // memory pipeline behind the other waves' stores (round 5's ablations:
-    // the 7 lock-path counter stores cost 9% of the step).  Only stores after
-    // a wave's last wait on a load: a store skipped on some path makes the
-    // compiler's vmcnt bookkeeping conservative for later loads.
-#ifndef ST_SKIP
-#define ST_SKIP 0
-#endif
-    constexpr bool SKIP = ST_SKIP && KSTEPS == 1;
-    constexpr bool EARLY = ST_EARLY && KSTEPS == 1 && !VEC && DO_L;
+    // st_step's wide packed obs path (16-B stores of 4-env groups, below)
     [[maybe_unused]] const bool wide_obs1 = OVP && (p.n & 3) == 0 && e0 + kWave <= p.n &&
                                             (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0 &&
                                             (!VEC || (reinterpret_cast<uintptr_t>(p.final_obs) & 15u) == 0);
-    // this lane's 4-env group (envs 4 (lane % 16) .. + 3) holds a locking env
-    [[maybe_unused]] const bool grp_lock = ((lockball >> (4 * (lane & 15))) & 0xFull) != 0;
-    if constexpr (EARLY) {
-        // the overlay of the non-locking lanes (the current piece); locking
-        // lanes write a dump slot (an address select, no branch)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            uint32_t *dst = &sm.OV[(ax + pc_dx(desc.y, j) + kPad) * kWave + lane];
-            *(locknow ? &sm.dump[lane] : dst) = pc_bits<S32>(desc.x, j, ay) & hmask;
-        }
-        const auto rr = buf_rsrc(p.reward, (uint32_t)p.n * 4u);
-        const auto rd = buf_rsrc(p.done, (uint32_t)p.n);
-        const bool now = real && !locknow;
-        __builtin_amdgcn_raw_buffer_store_b32(rew, rr, now ? (uint32_t)e * 4u : kOff, 0, kRD);
-        __builtin_amdgcn_raw_buffer_store_b8((char)0, rd, now ? (uint32_t)e : kOff, 0, kRD);
-        {
-            const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
-            const uint32_t eo = (uint32_t)e * 4u;
-            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)time, rs,
-                                                  !locknow ? eo + (uint32_t)ST_STAT_TIME * (uint32_t)sd * 4u : kOff, 0, kST);
-            __builtin_amdgcn_raw_buffer_store_b32(pack_piece(id, rot, ax, ay, lock), rs,
-                                                  !locknow ? eo + (uint32_t)kPieceRow * (uint32_t)sd * 4u : kOff, 0, kST);
-        }
-        wave_sync();
-        uint4 bw[NBQ], ow[NBQ];
-#pragma unroll
-        for (int q = 0; q < NBQ; ++q) {
-            if (WT || 4 * q < W) {
-                bw[q] = *reinterpret_cast<const uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]);
-                ow[q] = *reinterpret_cast<const uint4 *>(&sm.OV[(4 * q + lrow + kPad) * kWave + lcc]);
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        const auto ro = buf_rsrc(wide_obs1 ? p.obs : nullptr, (uint32_t)W * (uint32_t)p.n * 4u);
-#pragma unroll
-        for (int q = 0; q < NBQ; ++q) {
-            if (WT || 4 * q < W) {
-                const uint4 v = bw[q], o = ow[q];
-                const uint4 ob = make_uint4((v.x | o.x) & hmask, (v.y | o.y) & hmask, (v.z | o.z) & hmask,
-                                            (v.w | o.w) & hmask);
-                const uint32_t ooff = ((uint32_t)e0 + (uint32_t)(4 * q + lrow) * (uint32_t)p.n + (uint32_t)lcc) * 4u;
-                buf_store16<kNT>(ro, grp_lock ? kOff : ooff, ob);
-            }
-        }
-        ST_STAMP(9);  // (logic wave: the early stores issued)
-    }
 
     // ---------------- logic: lock path (tetris_env.py:263-299) ----------------
     bool died = false, spawn = false;
@@ -1603,17 +1527,6 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         }
     }
     ST_STAMP(3);
-    // SKIP_BOARD (round 6): the logic wave takes its late-loaded counters
-    // here, right after the lock path (issued before B1, they have long
-    // arrived), so that no load is waited on after its stores begin: every
-    // store from here on may then be skipped by a wave-uniform branch without
-    // making a later vmcnt wait conservative -- the board row groups no lane
-    // dirtied are not stored at all
-#ifndef ST_SKIP_BOARD
-#define ST_SKIP_BOARD 0
-#endif
-    constexpr bool SKIP_BOARD = ST_SKIP_BOARD && SKIP && LCL && DO_L;
-    if constexpr (SKIP_BOARD) asm volatile("" ::"v"(lcv[0]), "v"(lcv[1]), "v"(lcv[2]), "v"(lcv[3]), "v"(lcv[4]));
 
     const bool reset_now = died && p.autoreset == ST_AUTORESET_SAME_STEP;
     // a lock consumes the preview (spawn, or the same-step reset's new piece);
@@ -1635,77 +1548,11 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         // skipped on some path would make a later load's wait vmcnt(0).
         const auto rr = buf_rsrc(p.reward ? p.reward + (int64_t)t * p.n : nullptr, (uint32_t)p.n * 4u);
         const auto rd = buf_rsrc(p.done ? p.done + (int64_t)t * p.n : nullptr, (uint32_t)p.n);
-        const bool late = real && (!EARLY || locknow);  // EARLY: the other lanes stored theirs already
-        __builtin_amdgcn_raw_buffer_store_b32(rew, rr, late ? (uint32_t)e * 4u : kOff, 0, kRD);
-        __builtin_amdgcn_raw_buffer_store_b8((char)(died ? 1 : 0), rd, late ? (uint32_t)e : kOff, 0, kRD);
+        __builtin_amdgcn_raw_buffer_store_b32(rew, rr, real ? (uint32_t)e * 4u : kOff, 0, kRD);
+        __builtin_amdgcn_raw_buffer_store_b8((char)(died ? 1 : 0), rd, real ? (uint32_t)e : kOff, 0, kRD);
         if constexpr (KSTEPS == 1) ST_STAMP(10);  // (logic wave, round 6: reward / done stores issued)
     }
-    // OVL (round 6): the store phase with the overlay painted into the board
-    // plane itself and ONE transposed read -- half the LDS traffic of the
-    // overlay plane's (paint, keep / dirty masks, board rows and overlay
-    // rows, ~10 KB per wave, the phase's ~740 cycles in
-    // profiles/r06/stamps_fine_store_phase.txt).  The board rows then come
-    // from the obs rows: a locking env that spawned has row 0 empty under
-    // its new piece's visible cells (a spawn only overlays row 0, :277, :299),
-    // so its board is its obs with row 0 cleared; a same-step reset's board
-    // is empty; a non-locking env's board is unchanged and not stored -- so
-    // the board goes out as one dword per dirty env and row instead of 16-B
-    // groups of 4 envs.  A wave with a death without auto-reset (R8: the
-    // board is the obs minus the locked piece) takes the overlay-plane path.
-#ifndef ST_OVL
-#define ST_OVL 0
-#endif
-    constexpr bool OVL = ST_OVL && !EARLY && !VEC && KSTEPS == 1 && DO_L && LCL && WT != 0 && WT < 31;
-    if constexpr (OVL) asm volatile("" ::"v"(lcv[0]), "v"(lcv[1]), "v"(lcv[2]), "v"(lcv[3]), "v"(lcv[4]));
-    bool ovl_fast = false;
-    if constexpr (OVL) ovl_fast = !__ballot(died && !reset_now);
-    if (OVL && ovl_fast) {
-        uint2 pd = pd_pv;
-        const bool need1 = draw && !pv_ok(mt0);
-        if (__ballot(need1)) {
-            lds_flag_wait(&sm.f2, (uint32_t)t + 1u);
-            if (need1) pd = tab((int)sm.pick1[lane] * 4);
-        }
-        const uint32_t om = spawn ? pd.x : desc.x, og = spawn ? pd.y : desc.y;
-        const int ox = spawn ? W / 2 : ax, oy = spawn ? 0 : ay;
-        paint<S32>(L, lane, om, og, ox, oy, hmask);  // (a reset env's piece is in L already: idempotent)
-        // per env: the columns it changed | bit 31 = reset (empty board)
-        constexpr uint32_t kCols = (1u << (WT ? WT : 1)) - 1u;
-        sm.BD[lane] = (died ? kCols : (bdirty & kCols)) | (reset_now ? 0x80000000u : 0u);
-        wave_sync();
-        const uint4 fl4 = *reinterpret_cast<const uint4 *>(&sm.BD[lcc]);
-        uint4 rw[NBQ];
-#pragma unroll
-        for (int q = 0; q < NBQ; ++q) rw[q] = *reinterpret_cast<const uint4 *>(&L[(4 * q + lrow + kPad) * kWave + lcc]);
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (STAMP) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            ST_STAMP(11);
-        }
-        const auto ro = buf_rsrc(wide_obs1 ? p.obs : nullptr, (uint32_t)W * (uint32_t)p.n * 4u);
-        const auto rb = buf_rsrc(p.board, (uint32_t)W * (uint32_t)sd * 4u);
-        const uint32_t boff = ((uint32_t)e0 * 4u + loff * 4u);
-        const uint32_t fa[4] = {fl4.x, fl4.y, fl4.z, fl4.w};
-#pragma unroll
-        for (int q = 0; q < NBQ; ++q) {
-            const uint4 v = rw[q];
-            const uint4 ob = make_uint4(v.x & hmask, v.y & hmask, v.z & hmask, v.w & hmask);
-            const uint32_t ooff = ((uint32_t)e0 + (uint32_t)(4 * q + lrow) * (uint32_t)p.n + (uint32_t)lcc) * 4u;
-            buf_store16<kNT>(ro, ooff, ob);
-            const uint32_t va[4] = {ob.x, ob.y, ob.z, ob.w};
-            const int x = 4 * q + lrow;  // board row (column x of the reference's board)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const bool dirty = x < W && ((fa[i] >> x) & 1u) && !(kAblate & 4096u);
-                const uint32_t keep = (fa[i] >> 31) ? 0u : ~1u;  // reset: empty; spawn: row 0 cleared
-                __builtin_amdgcn_raw_buffer_store_b32(va[i] & keep, rb,
-                                                      dirty ? boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u + 4u * (uint32_t)i
-                                                            : kOff,
-                                                      0, kST);
-            }
-        }
-    }
-    if (DO_L && KSTEPS == 1 && !(OVL && ovl_fast)) {
+    if constexpr (DO_L && KSTEPS == 1) {
         // The post-step board never depends on the spawned piece either (a
         // spawn only overlays row 0, which is empty after a non-fatal lock,
         // :277), so st_step stores it here: non-locking lanes and spawns: L; a
@@ -1732,12 +1579,8 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             const uint32_t om = spawn ? pd.x : desc.x, og = spawn ? pd.y : desc.y;
             const int ox = spawn ? W / 2 : ax, oy = spawn ? 0 : ay;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                // (EARLY: the non-locking lanes painted theirs before the lock path)
-                uint32_t *dst = &sm.OV[(ox + pc_dx(og, j) + kPad) * kWave + lane];
-                if constexpr (EARLY) dst = locknow ? dst : &sm.dump[lane];
-                if (!(kAblate & 4194304u)) *dst = pc_bits<S32>(om, j, oy) & hmask;
-            }
+            for (int j = 0; j < 4; ++j)  // (ablation 4194304: skipped, timing only)
+                if (!(kAblate & 4194304u)) sm.OV[(ox + pc_dx(og, j) + kPad) * kWave + lane] = pc_bits<S32>(om, j, oy) & hmask;
         }
         uint4 km, bd4;
         uint4 bw[NBQ], ow[NBQ];
@@ -1808,8 +1651,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                         const uint4 keep = p.final_obs ? km : make_uint4(~0u, ~0u, ~0u, ~0u);
                         buf_store16<kNT>(ro, ooff, make_uint4(ob.x & keep.x, ob.y & keep.y, ob.z & keep.z, ob.w & keep.w));
                     } else {
-                        // (EARLY: groups without a locking env went out before the lock path)
-                        buf_store16<kNT>(ro, EARLY && !grp_lock ? kOff : ooff, ob);
+                        buf_store16<kNT>(ro, ooff, ob);
                     }
                 }
                 v.x &= km.x;
@@ -1818,8 +1660,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
                 v.w &= km.w;
                 // row 4q + lrow; padding rows (>= W) are never dirty
                 const bool dirty = ((bdl >> (4 * q)) & 1u) && 4 * q + lrow < W && !(kAblate & 4096u);
-                if (!SKIP_BOARD || __ballot(dirty))
-                    buf_store16<kST>(rb, dirty ? boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff, v);
+                buf_store16<kST>(rb, dirty ? boff + (uint32_t)(4 * q) * (uint32_t)sd * 4u : kOff, v);
             }
         }
         // (below: the ragged / unaligned obs path and the float32 writer read
@@ -1871,7 +1712,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         // this step's next-generation chunk (its operands arrived long ago);
         // its env's progress advances unless that env's own draw switched
         // generations (finishing the successor itself: same words)
-        const int chunk_pg = mt_chunk_store<KSTEPS == 1 ? kST : 0, SKIP>(mrs, lane, chunk);
+        const int chunk_pg = mt_chunk_store<KSTEPS == 1 ? kST : 0>(mrs, lane, chunk);
         const bool chunk_me = lane == chunk.l;
         ST_STAMP(4);
         if constexpr (STAMP) {  // 1: a draw started a generation, 2: a draw ran past its 8 words
@@ -1905,12 +1746,10 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             const bool cst = !(kAblate & (2048u | 32768u));
             const bool mst = cst && !(kAblate & 131072u) && (dr || chunk_me);
             const bool kst = cst && !(kAblate & 65536u) && dr;
-            if (!SKIP || __ballot(mst))
-                __builtin_amdgcn_raw_buffer_store_b32(
-                    mt_out, rs, mst ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff, 0, kST);
-            if (!SKIP || __ballot(kst))
-                __builtin_amdgcn_raw_buffer_store_b32(
-                    (uint32_t)csid, rs, kst ? eo + (uint32_t)(ST_STAT_COUNT0 + sid) * (uint32_t)sd * 4u : kOff, 0, kST);
+            __builtin_amdgcn_raw_buffer_store_b32(mt_out, rs, mst ? eo + (uint32_t)ST_STAT_MT_INDEX * (uint32_t)sd * 4u : kOff,
+                                                  0, kST);
+            __builtin_amdgcn_raw_buffer_store_b32(
+                (uint32_t)csid, rs, kst ? eo + (uint32_t)(ST_STAT_COUNT0 + sid) * (uint32_t)sd * 4u : kOff, 0, kST);
             if constexpr (VEC) {  // st_step_vec's info snapshot: the shape counts after the step
                 const auto ri = buf_rsrc(p.info, (uint32_t)ST_NSTAT * (uint32_t)p.n * 4u);
 #pragma unroll
@@ -1986,14 +1825,11 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
             const auto rs = buf_rsrc(p.stats, (uint32_t)kHotRows * (uint32_t)sd * 4u);
             const uint32_t eo = (uint32_t)e * 4u;
             auto put = [&](int r, int32_t v, bool on) {
-                if constexpr (SKIP) {
-                    if (!__ballot(on)) return;  // no lane changed this row: no store instruction
-                }
                 __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, rs, on ? eo + (uint32_t)r * (uint32_t)sd * 4u : kOff,
                                                       0, kST);
             };
-            put(ST_STAT_TIME, time, !EARLY || locknow);  // (EARLY: the others went out before the lock path)
-            put(kPieceRow, (int32_t)pw_out, !EARLY || locknow);
+            put(ST_STAT_TIME, time, true);
+            put(kPieceRow, (int32_t)pw_out, true);
             const bool cst = !(kAblate & (2048u | 16384u));  // (ablation: lock-path counter stores dropped)
             put(ST_STAT_SCORE, score, cst && locknow && score != o_score);
             put(ST_STAT_LINES, lines, cst && locknow && lines != o_lines);
@@ -2181,9 +2017,7 @@ __device__ __forceinline__ void run_steps(const KParams &p, StepLds<WT, F32, KST
         // st_set_action_flag's sticky word: only lanes that saw a bad action
         // store (a raw buffer store with an out-of-range offset elsewhere, no
         // branch); a null flag has an empty range, so nothing is written
-        // (SKIP: the store is issued only in a wave that saw a bad action)
-        if (!(ST_SKIP && KSTEPS == 1) || __ballot(bad_act))
-            __builtin_amdgcn_raw_buffer_store_b32(1u, buf_rsrc(p.act_flag, 4u), bad_act ? 0u : kOff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(1u, buf_rsrc(p.act_flag, 4u), bad_act ? 0u : kOff, 0, 0);
     }
     if constexpr (KSTEPS != 1 && DO_L) {
         // 32-bit buffer offsets: 64-bit row offsets shared with the prologue
@@ -3080,16 +2914,8 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
             if (lane == last_l && cur == last_cur && last_pg > pg) pg = last_pg;
             mt_chunk_issue_pc(orm, (w >> 31) != 0u && pg < kMtN, pg, cur, lane, ch);
         };
-        // RO_SKIP (round 6): the output wave issues the chunk's pad-copy store
-        // and a step's episode-counter stores only in waves where a lane
-        // needs them (wave-uniform branches), after the chunk's operand
-        // wait, so every vmcnt count stays exact
-#ifndef ST_RO_SKIP
-#define ST_RO_SKIP 0
-#endif
-        constexpr bool RO_SKIP = ST_RO_SKIP;
         auto chunk_done = [&]() {
-            const int npg = mt_chunk_store<0, RO_SKIP>(orm, lane, ch);
+            const int npg = mt_chunk_store<0>(orm, lane, ch);
             if (ch.l >= 0) {
                 last_l = ch.l;
                 last_cur = ch.cur;
@@ -3218,48 +3044,32 @@ __device__ __forceinline__ void rollout_wave(const KParams &p, RoLds<WT, F32> &s
                             *reinterpret_cast<uint4 *>(&OV[(4 * q + lrow + kPad) * kWave + lcc]) =
                                 make_uint4(0u, 0u, 0u, 0u);
                 }
-                // a reset's episode counters of step t (read from the hand-off
-                // buffer before fq is raised; stored below)
-                const uint32_t dn = sm.dn[t & 1][lane];
-                const bool rs_now = dn != 0u && p.autoreset == ST_AUTORESET_SAME_STEP;
-                uint32_t epv[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) epv[k] = sm.ep[t & 1][k][lane];
                 {
-                    // reward / done of step t: branch-free stores, out-of-range
-                    // offsets where there is nothing to store
+                    // reward / done of step t (and a reset's episode counters): branch-free
+                    // stores, out-of-range offsets where there is nothing to store
                     const auto rr = buf_rsrc(p.reward ? p.reward + (int64_t)t * p.n : nullptr, (uint32_t)p.n * 4u);
                     const auto rd = buf_rsrc(p.done ? p.done + (int64_t)t * p.n : nullptr, (uint32_t)p.n);
+                    const uint32_t dn = sm.dn[t & 1][lane];
                     if (!(kAblate & 64u)) {
                         __builtin_amdgcn_raw_buffer_store_b32(sm.rw[t & 1][lane], rr, real ? (uint32_t)e * 4u : kOff, 0, kRD);
                         __builtin_amdgcn_raw_buffer_store_b8((char)dn, rd, real ? (uint32_t)e : kOff, 0, kRD);
+                        const bool rs_now = dn != 0u && p.autoreset == ST_AUTORESET_SAME_STEP;
+                        const auto rs = buf_rsrc(p.stats, (uint32_t)ST_NSTAT * (uint32_t)sd * 4u);
+                        const uint32_t eo = (uint32_t)e * 4u;
+                        constexpr int kEpRow[4] = {ST_STAT_EP_TIME, ST_STAT_EP_SCORE, ST_STAT_EP_LINES, ST_STAT_EP_HOLES};
+#pragma unroll
+                        for (int k = 0; k < 4; ++k)
+                            __builtin_amdgcn_raw_buffer_store_b32(sm.ep[t & 1][k][lane], rs,
+                                                                  rs_now ? eo + (uint32_t)kEpRow[k] * (uint32_t)sd * 4u : kOff, 0, kST);
                     }
                 }
-                auto ep_store = [&]() {
-                    if (kAblate & 64u) return;
-                    if constexpr (RO_SKIP) {
-                        if (!__ballot(rs_now)) return;  // no env of the wave was reset in step t
-                    }
-                    const auto rs = buf_rsrc(p.stats, (uint32_t)ST_NSTAT * (uint32_t)sd * 4u);
-                    const uint32_t eo = (uint32_t)e * 4u;
-                    constexpr int kEpRow[4] = {ST_STAT_EP_TIME, ST_STAT_EP_SCORE, ST_STAT_EP_LINES, ST_STAT_EP_HOLES};
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        __builtin_amdgcn_raw_buffer_store_b32(epv[k], rs,
-                                                              rs_now ? eo + (uint32_t)kEpRow[k] * (uint32_t)sd * 4u : kOff, 0, kST);
-                };
-                if constexpr (!RO_SKIP) ep_store();
                 if constexpr (!EARLY)
                     if (lane == 0) lds_flag_set(&sm.fq, (uint32_t)t + 1u);  // the logic wave may change the planes
                 stamp(4);
                 if constexpr (CHO) {
                     if constexpr (decltype(dn_c)::value) chunk_done();  // the previous chunk (none at first: ch.l < 0)
                     stamp(5);
-                    // (RO_SKIP: after the chunk's operand wait, before the next chunk's loads)
-                    if constexpr (RO_SKIP) ep_store();
                     if constexpr (decltype(nx_c)::value) chunk_next();
-                } else if constexpr (RO_SKIP) {
-                    ep_store();
                 }
                 stamp(2);
             };

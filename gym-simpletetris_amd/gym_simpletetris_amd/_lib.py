@@ -17,7 +17,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ST_LIB") or os.path.join(_HERE, "libsimpletetris.so")
 
 ST_OK, ST_EINVAL, ST_ENOMEM, ST_EHIP, ST_ESTATE = 0, -1, -2, -3, -4
-ABI_VERSION = 3  # ST_ABI_VERSION of include/simpletetris.h
+ABI_VERSION = 4  # ST_ABI_VERSION of include/simpletetris.h
 
 # st_flags (include/simpletetris.h) keyed by the reference kwarg names
 # (TetrisEngine.__init__, tetris_env.py:126-137).
@@ -40,7 +40,7 @@ NSTAT = 19
 MT_N = 624
 EXPORT_MT, EXPORT_OBS_F32 = 1, 2  # st_export_env parts
 
-EXPORTS = ("st_create", "st_destroy", "st_seed", "st_reset", "st_step", "st_step_f32", "st_step_vec", "st_rollout",
+EXPORTS = ("st_create", "st_destroy", "st_seed", "st_reset", "st_step", "st_step_f32", "st_step_n", "st_step_vec", "st_rollout",
            "st_wire_words", "st_step_wire", "st_unwire", "st_unwire_shards",
            "st_obs_to_f32", "st_render", "st_grayscale", "st_state", "st_copy", "st_mt_sync", "st_state_bytes", "st_save",
            "st_load", "st_export_env", "st_export_words", "st_check_actions", "st_set_action_flag", "st_gate_actions",
@@ -91,6 +91,7 @@ def load(path: str = LIB_PATH):
         "st_reset": ([vp, vp, vp], ctypes.c_int),
         "st_step": ([vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "st_step_f32": ([vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
+        "st_step_n": ([vp, vp, ctypes.c_int64, vp, vp, vp, vp, vp], ctypes.c_int),
         "st_step_vec": ([vp, vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "st_rollout": ([vp, i32, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "st_wire_words": ([i32, i32], ctypes.c_int),

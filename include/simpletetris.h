@@ -33,9 +33,9 @@ extern "C" {
 
 /* 2: st_step_wire carries the reward's 32 bits (st_wire_words grew by one
  * word for 10x20), st_unwire_shards.  3: st_gate_actions / st_gate_wait,
- * st_stream_wait (additions only).  Snapshots (st_save) keep their own
- * format version, unchanged. */
-#define ST_ABI_VERSION 3
+ * st_stream_wait (additions only).  4: st_step_n (addition only).
+ * Snapshots (st_save) keep their own format version, unchanged. */
+#define ST_ABI_VERSION 4
 
 typedef struct st_ctx st_ctx;
 typedef void *st_stream; /* hipStream_t */
@@ -153,6 +153,17 @@ int st_step(st_ctx *ctx, const uint8_t *d_actions, uint32_t *d_obs, int32_t *d_r
  * fused into the step kernel. */
 int st_step_f32(st_ctx *ctx, const uint8_t *d_actions, uint32_t *d_obs, float *d_obs_f32,
                 int32_t *d_reward, uint8_t *d_done, st_stream stream);
+
+/* k consecutive steps (TetrisEngine.step k times, :243-304), one step
+ * kernel launch each, enqueued by one host call: step i takes the actions at
+ * device pointer d_actions[i] (d_actions: a HOST array of k device
+ * pointers) and writes d_obs / d_obs_f32 (NULL: packed only) / d_reward /
+ * d_done, so each holds step k-1's outputs when the stream reaches the end
+ * -- st_step / st_step_f32 called k times, without the caller's per-call
+ * host overhead between the launches (a native driver loop).  An armed
+ * st_gate_actions gates the first of the k steps only.  k <= 0: nothing. */
+int st_step_n(st_ctx *ctx, const uint8_t *const *d_actions, int64_t k, uint32_t *d_obs, float *d_obs_f32,
+              int32_t *d_reward, uint8_t *d_done, st_stream stream);
 
 /* st_step for a vector env (gym's autoreset convention), one
  * launch.  d_obs_f32 may be NULL (packed only).

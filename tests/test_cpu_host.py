@@ -36,7 +36,7 @@ def test_host_only_abi_functions_and_constants():
     the Python binding mirrors."""
     from gym_simpletetris_amd import _lib
     L = _lib.load()
-    assert L.st_abi_version() == _lib.ABI_VERSION == 3
+    assert L.st_abi_version() == _lib.ABI_VERSION == 4
     assert L.st_export_words(10, 20) == 10 + 2 + _lib.NSTAT + _lib.MT_N + 200
     assert L.st_export_words(4, 4) == 4 + 2 + _lib.NSTAT + _lib.MT_N + 16
     # the C5 gather format: ceil((W*H + 17) / 32) words per env
@@ -51,6 +51,7 @@ def test_host_only_abi_functions_and_constants():
     # argument checks that return before any GPU call
     assert L.st_gate_actions(None, None, None) == _lib.ST_EINVAL
     assert L.st_gate_wait(None) == _lib.ST_EINVAL
+    assert L.st_step_n(None, None, 3, None, None, None, None, None) == _lib.ST_EINVAL
     assert L.st_stream_wait(None, None) == _lib.ST_OK  # a stream never waits for itself
 
 

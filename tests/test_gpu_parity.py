@@ -1293,3 +1293,42 @@ def test_host_written_large_shape_counts(mode):
     for i in range(n):
         assert list(fin["stats"][6:13, i].astype(np.int64)) == list(np.ctypeslib.as_array(ob.envs[i].counts)), i
         assert int(fin["stats"][13, i]) == ob.envs[i].rng.index, i
+
+
+def test_step_n_equals_k_step_calls():
+    """st_step_n (ABI 4, the bench's native launch loop): k steps enqueued by
+    one call -- step i with the actions at d_actions[i] -- leave the same
+    state and last-step outputs as k st_step calls, packed and float32;
+    k = 0 enqueues nothing."""
+    import ctypes
+    G = _engine()
+    n, k = 3000, 37
+    for f32 in (False, True):
+        a = G.TetrisBatch(n, seeds=range(n), autoreset="same_step", validate_actions=False)
+        b = G.TetrisBatch(n, seeds=range(n), autoreset="same_step", validate_actions=False)
+        a.reset()
+        b.reset()
+        acts = torch.stack([b.gen_actions(t, 11) for t in range(k)])
+        vp = ctypes.c_void_p
+        arr = (vp * k)(*[acts[t].data_ptr() for t in range(k)])
+        o = torch.zeros((10, n), dtype=torch.int32, device=a.device)
+        r = torch.zeros(n, dtype=torch.int32, device=a.device)
+        d = torch.zeros(n, dtype=torch.uint8, device=a.device)
+        f = torch.zeros((n, 10, 20), dtype=torch.float32, device=a.device) if f32 else None
+        s = vp(torch.cuda.current_stream().cuda_stream)
+        assert a._L.st_step_n(a._ctx, vp(ctypes.addressof(arr)), 0, vp(o.data_ptr()), None, vp(r.data_ptr()),
+                              vp(d.data_ptr()), s) == 0
+        assert a._L.st_step_n(a._ctx, vp(ctypes.addressof(arr)), k, vp(o.data_ptr()),
+                              vp(f.data_ptr()) if f32 else None, vp(r.data_ptr()), vp(d.data_ptr()), s) == 0
+        for t in range(k):
+            ob, rb, db = b.step(acts[t], obs="f32" if f32 else "packed")
+        torch.cuda.synchronize()
+        if f32:
+            assert torch.equal(f, ob)
+            ob = b.obs
+        assert torch.equal(o, ob) and torch.equal(r, rb) and torch.equal(d.bool(), db.bool())
+        sa, sb = a.get_state(("board", "stats", "mt")), b.get_state(("board", "stats", "mt"))
+        for key in sa:
+            assert np.array_equal(sa[key], sb[key]), (key, f32)
+        a.close()
+        b.close()
