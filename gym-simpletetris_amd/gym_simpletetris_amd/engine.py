@@ -410,6 +410,34 @@ class TetrisBatch:
                                        _ptr(d), self._stream()))
         return (f if obs == "f32" else o), r, d
 
+    def step_n(self, actions: torch.Tensor, obs: str = "packed"):
+        """K consecutive steps, one st_step kernel launch each, enqueued by
+        ONE library call (st_step_n: the launch loop runs in C, with no
+        Python between the launches).  actions: uint8 [K, n] on the device
+        (checked like rollout()'s).  Identical to K calls of step(); returns
+        the LAST step's (obs, reward, done) in the engine's reused buffers
+        ('packed': int32 [W, n], 'f32': float32 [n, W, H], 'none': None)."""
+        actions = _from_dlpack(actions)
+        if not isinstance(actions, torch.Tensor) or actions.dim() != 2 or actions.shape[1] != self.n \
+                or actions.shape[0] < 1:
+            raise ValueError(f"actions must be a [K, {self.n}] integer tensor")
+        if obs not in ("packed", "f32", "none"):
+            raise ValueError("obs: 'packed', 'f32' or 'none'")
+        K = int(actions.shape[0])
+        actions = self._actions(actions, lead=(K,))
+        if obs == "f32" and self.obs_f32 is None:
+            self.obs_f32 = torch.zeros((self.n, self.width, self.height), dtype=torch.float32, device=self.device)
+        row = actions.stride(0)
+        base = actions.data_ptr()
+        ptrs = (ctypes.c_void_p * K)(*[base + t * row for t in range(K)])
+        C.check(self._L.st_step_n(self._ctx, ctypes.addressof(ptrs), K,
+                                  _ptr(self.obs) if obs != "none" else None,
+                                  _ptr(self.obs_f32) if obs == "f32" else None,
+                                  _ptr(self.reward), _ptr(self.done), self._stream()))
+        if obs == "f32":
+            return self.obs_f32, self.reward, self.done
+        return (self.obs if obs == "packed" else None), self.reward, self.done
+
     # ------------------------------------------------------------ observations
     def obs_to_f32(self, packed: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Packed obs -> float32 [n][W][H] (the reference's np.float32 board)."""

@@ -1332,3 +1332,37 @@ def test_step_n_equals_k_step_calls():
             assert np.array_equal(sa[key], sb[key]), (key, f32)
         a.close()
         b.close()
+
+
+@pytest.mark.parametrize("obs", ["packed", "f32", "none"])
+def test_engine_step_n_equals_step_calls(obs):
+    """TetrisBatch.step_n (st_step_n behind it): K rows of actions, the last
+    step's outputs and every env's state as K step() calls; a bad action
+    raises KeyError before any step with validate_actions=True."""
+    G = _engine()
+    n, k = 1500, 23
+    a = G.TetrisBatch(n, seeds=range(n), autoreset="same_step", validate_actions=True)
+    b = G.TetrisBatch(n, seeds=range(n), autoreset="same_step", validate_actions=False)
+    a.reset()
+    b.reset()
+    acts = torch.stack([b.gen_actions(t, 5) for t in range(k)])
+    oa, ra, da = a.step_n(acts, obs=obs)
+    for t in range(k):
+        ob, rb, db = b.step(acts[t], obs=obs)
+    torch.cuda.synchronize()
+    assert (oa is None) == (ob is None) and (oa is None or torch.equal(oa, ob))
+    assert torch.equal(ra, rb) and torch.equal(da, db)
+    sa, sb = a.get_state(("board", "stats", "mt")), b.get_state(("board", "stats", "mt"))
+    for key in sa:
+        assert np.array_equal(sa[key], sb[key]), key
+    bad = acts.clone()
+    bad[3, 7] = 9
+    before = a.get_state(("board", "stats", "mt"))
+    before = {key: v.copy() for key, v in before.items()}
+    with pytest.raises(KeyError):
+        a.step_n(bad, obs=obs)
+    after = a.get_state(("board", "stats", "mt"))
+    for key in before:
+        assert np.array_equal(before[key], after[key]), key
+    a.close()
+    b.close()
